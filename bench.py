@@ -1,0 +1,227 @@
+"""Benchmark: clips/s forward+backward of the SCA hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE config 2, the metric's configuration): four keypoint streams
+(body/left/right/face = 6/21/21/31 of K=79 joints) sliced out of one (B=8, T=256, 79, 2)
+synthetic keypoint batch, each through coordinate mapping + the 4-layer SCA stack
+(d=256, 16 heads, ff 768), forward + backward of every parameter.  One "step" = one such
+fwd+bwd over the batch; with N > 1 GPUs each rank runs its own 8 clips (weak scaling) and
+the step includes the RCCL gradient all-reduce.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2] [--no-graph]
+
+Prints ONE JSON line on rank 0 (contract in the build instructions), including:
+  roofline      the dominant kernel's algorithmic FLOP rate (HIP events around each of its
+                launches in an instrumented eager step after the timed region) vs fp32 MFMA peak
+  cpu_baseline  the CPU oracle (plain PyTorch fp32 restatement) timed on this host's cores
+                on a bounded sample of the same workload (rank 0, N = 1 only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from scattennet_amd import ops, workloads as W  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA == fp32 vector peak
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(W.WORKLOADS))
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one captured hipGraph")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU-oracle baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+class GradAllReduce:
+    """Data parallelism over RCCL: gradients are averaged across ranks with ONE coalesced
+    fp32 all-reduce per step (flat buffer; the 4-stream SCA has 25.8 M params = 103 MB).
+    The reference has no DP at all — this is the north-star's batch-sharded
+    data parallelism, oracle: the single-process gradient of the full batch."""
+
+    def __init__(self, params, world):
+        self.params = [p for p in params if p.requires_grad]
+        self.world = world
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=self.params[0].device, dtype=torch.float32)
+
+    def __call__(self):
+        if self.world == 1:
+            return
+        o = 0
+        views = []
+        for p in self.params:
+            k = p.numel()
+            v = self.flat[o:o + k]
+            if p.grad is None:
+                v.zero_()
+            else:
+                v.copy_(p.grad.reshape(-1))
+            views.append((p, v))
+            o += k
+        dist.all_reduce(self.flat)
+        self.flat.mul_(1.0 / self.world)
+        for p, v in views:
+            if p.grad is not None:
+                p.grad.copy_(v.view_as(p.grad))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    w = W.WORKLOADS[args.workload]
+
+    model = W.build_streams(w, dev, seed=0, init="reference")
+    if world > 1:  # identical initial weights on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    kp, mask, gout = W.synthetic_batch(w, dev, seed=1 + rank)
+    grads_out = [gout[g].contiguous() for g in range(len(w["groups"]))]
+    allreduce = GradAllReduce(model.parameters(), world)
+    params = [p for p in model.parameters()]
+
+    def step():
+        outs = model(kp, mask)
+        torch.autograd.backward(outs, grads_out)
+        allreduce()
+
+    # warm-up (also builds the library's lazy state) on a side stream, as graph capture requires
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(max(1, args.warmup)):
+            for p in params:
+                p.grad = None
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+
+    graph = None
+    if not args.no_graph:
+        for p in params:
+            p.grad = None
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        for _ in range(2):
+            graph.replay()
+        torch.cuda.synchronize()
+
+    def run(k):
+        for _ in range(k):
+            if graph is not None:
+                graph.replay()
+            else:
+                for p in params:
+                    p.grad = None
+                step()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = 1000.0 * elapsed / args.steps
+    clips = w["B"] * world * args.steps / elapsed
+    step_flops = W.flops_per_step(w)
+
+    # ---- dominant-kernel roofline: one instrumented eager step (HIP events per launch) ----
+    prof = ops.LaunchProfiler()
+    with prof:
+        for p in params:
+            p.grad = None
+        step()
+    torch.cuda.synchronize()
+    kname, kstat = prof.dominant()
+    achieved = kstat["flops"] / kstat["seconds"] / 1e12 if kstat["seconds"] > 0 else 0.0
+    roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "launches": kstat["launches"], "avg_launch_us": round(1e6 * kstat["seconds"] / kstat["launches"], 2),
+                "flops_per_launch": kstat["flops"] / kstat["launches"],
+                "step_achieved": round(step_flops / (ms / 1e3) / 1e12, 3),
+                "step_frac": round(step_flops / (ms / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(w, model, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "clips/sec fwd+bwd, (B=8,T=256,K=79,d=256) at 1/2/4/8 MI355X",
+            "value": round(clips, 2), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (U[0,1) keypoints, MSCA_Net init)",
+            "config": {"workload": f"{args.workload}: " + describe(w), "clips_per_gpu": w["B"], "frames": w["T"],
+                       "joints": w["K_all"], "streams": w["groups"], "d_model": w["d"], "heads": w["H"],
+                       "layers": w["L"], "dropout": 0.0, "hipgraph": graph is not None,
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def describe(w):
+    return (f"{len(w['groups'])}-stream SCA (mapping + {w['L']}x self / causal / cross-merge), "
+            f"B={w['B']} T={w['T']} K={w['K_all']} d={w['d']} H={w['H']}, fwd+bwd all params")
+
+
+def cpu_baseline(w, model, budget_s):
+    """The CPU oracle (oracle/sca_oracle.py, pinned to the reference's golden vectors) timed
+    on this host: same workload, same weights, a bounded number of fwd+bwd iterations."""
+    from oracle import sca_oracle as O
+    threads = os.cpu_count() or 1
+    # the GPU box reports the whole machine; use the box's CPU share (16) at most
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+    torch.set_num_threads(threads)
+    cfg = W.model_cfg(w["d"], w["H"], w["L"], maxpos=w["maxpos"])
+    groups = W.split_groups(w["groups"])
+    plist = [{k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+             for m in model.streams]
+    kp, mask, gout = W.synthetic_batch(w, "cpu", seed=1)
+    iters = 0
+    t0 = time.perf_counter()
+    while True:
+        outs = O.multi_stream_sca(plist, kp, mask, groups, cfg)
+        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+        for p in plist:
+            for v in p.values():
+                v.grad = None
+        iters += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(w["B"] * iters / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} fwd+bwd step(s) of the full workload (B={w['B']}) on the CPU oracle, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

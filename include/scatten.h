@@ -1,0 +1,241 @@
+/*
+ * scatten.h — C ABI of libscatten_hip.so, the MI355X (gfx950) implementation of the
+ * SCAttenNet spatial-coordinate-attention hot path.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t (passed as
+ * void*), never allocates, never synchronises, and is safe under hipGraph stream capture.
+ * Each returns 0 on success or a nonzero SCA_ERR_* code (the Python layer maps it to an
+ * exception; sca_last_error() gives the message).  All floating point is fp32.
+ *
+ * Reference interfaces replaced (tinh2044/SCAttenNet @ 2025-07-18; the reference is pure
+ * PyTorch, so each entry point replaces an ATen op sequence, not a reference kernel):
+ *   sca_gemm               nn.Linear forward/backward in model/attention.py:23-26,41-44,
+ *                          49-51,74,101-103,126 ; model/layers.py:97-99,106-108 ;
+ *                          model/fusion.py:31-34 ; model/residual.py:14-19
+ *                          (q-scaling after bias :49, v-from-kv/2 :103, GELU :98 fused)
+ *   sca_attn_fwd           attention.py:63-72 (SelfAttention), :115-124 (CrossAttention),
+ *                          :165-178 (SelfCausalAttention) incl. model/utils.py:3-28 masks
+ *   sca_attn_bwd           autograd of the same three op sequences
+ *   sca_layernorm_fwd/bwd  nn.LayerNorm + the residual add in keypoint_module.py:67-72,
+ *                          :101-111 and the position embedding add layers.py:15-30
+ *   sca_reduce_rows        bias / LayerNorm-affine / position-table gradient reductions
+ *   sca_coord_map_fwd/bwd  KeypointModule stream slicing + CoordinateMapping
+ *                          (model/__init__.py:133-142, keypoint_module.py:22-26,
+ *                          layers.py:111-123)
+ */
+#ifndef SCATTEN_H
+#define SCATTEN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCA_OK 0
+#define SCA_ERR_ARG 1      /* invalid shape / alignment / argument */
+#define SCA_ERR_LAUNCH 2   /* hipLaunchKernel failed */
+
+#define SCA_GEMM_MAX_PROBLEMS 12
+#define SCA_GEMM_MAX_SEGS 3
+
+/* GEMM layouts: C[M,N] = sum_seg alpha_s * op(A_s) op(B_s)                           */
+#define SCA_GEMM_NT 0  /* A[M,K] row-major, B[N,K] row-major  (Linear forward)          */
+#define SCA_GEMM_NN 1  /* A[M,K] row-major, B[K,N] row-major  (Linear dX = dY W)        */
+#define SCA_GEMM_TN 2  /* A[K,M] row-major, B[K,N] row-major  (Linear dW = dY^T X)      */
+
+/* Epilogue flags (applied in this order):
+ *   v = acc ; v += bias[n] ; v *= post_scale ;
+ *   GELU : aux_out[m,n] = v ; v = gelu_erf(v)
+ *   DGELU: v *= gelu_erf'(aux[m,n])
+ *   v += resid[m,n] (if resid) ; ACCUM: v += C[m,n] ; C[m,n] = v                     */
+#define SCA_EPI_GELU 1
+#define SCA_EPI_DGELU 2
+#define SCA_EPI_ACCUM 4
+
+typedef struct {
+  const float* A;
+  const float* B;
+  int lda, ldb;
+  int K;       /* reduction length of this segment (multiple of 4) */
+  float alpha; /* scales A on load: alpha=0.5 reproduces v_proj(kv/2) exactly */
+} sca_gemm_seg;
+
+typedef struct {
+  sca_gemm_seg seg[SCA_GEMM_MAX_SEGS];
+  int nseg;
+  int M, N;
+  float* C;
+  int ldc;
+  int epi;
+  const float* bias; /* [N] or NULL */
+  float post_scale;
+  const float* resid; /* [M, ldr] or NULL */
+  int ldr;
+  const float* aux; /* DGELU input [M, ldx] */
+  int ldx;
+  float* aux_out; /* GELU pre-activation output [M, ldo] */
+  int ldo;
+} sca_gemm_problem;
+
+/* Grouped GEMM over `nprob` independent problems (e.g. q/k/v x streams).
+ * splitk > 1 (TN layout, single segment only) writes fp32 partial slabs into
+ * `workspace` (nprob * splitk * M * N floats, problems must share M and N) and reduces
+ * them in a second launch in fixed order (deterministic).                               */
+int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+             void* stream);
+
+/* Fused masked attention over (B, T, H*hd) row-major activations (head h at columns
+ * h*hd .. h*hd+hd-1, row stride ld*).  Scores use q as given (the projection already
+ * applied hd^-0.5).  Masking, per query row i and key j:
+ *   causal && j > i                    -> -inf            (attention.py:165-169)
+ *   add_mask != NULL                   -> s + add_mask[b, i, j]   (general (B,1,Tq,Tk))
+ *   else key_valid != NULL && !valid_j -> finfo.min       (utils.py:3-12)
+ *   else                               -> s + (causal && plus_one ? 1 : 0) (utils.py:24-27)
+ * Softmax stats are saved per (g,b,h,i) as m (row max) and ll (log of the row sum) so
+ * that fully padded rows (all finfo.min) recompute to exactly uniform weights.         */
+typedef struct {
+  const float* q;
+  const float* k;
+  const float* v;
+  float* o;
+  float* stat_m;  /* [B*H*Tq] */
+  float* stat_ll; /* [B*H*Tq] */
+  const float* key_valid; /* [B, Tk] 1.0/0.0, or NULL */
+  const float* add_mask;  /* [B, Tq, Tk] additive, or NULL */
+} sca_attn_fwd_problem;
+
+typedef struct {
+  const float* q;
+  const float* k;
+  const float* v;
+  const float* o;
+  const float* dout;
+  const float* stat_m;
+  const float* stat_ll;
+  const float* key_valid;
+  const float* add_mask;
+  float* dq;    /* written (not accumulated), scaled by dq_scale */
+  float* dk;
+  float* dv;
+  float* delta; /* workspace [B*H*Tq] : rowsum(dO * O) */
+  float dq_scale;
+  float dv_scale;
+} sca_attn_bwd_problem;
+
+#define SCA_ATTN_MAX_PROBLEMS 8
+
+int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B, int H, int Tq, int Tk, int hd,
+                 int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream);
+int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B, int H, int Tq, int Tk, int hd,
+                 int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream);
+
+/* y = act(LayerNorm(x + r) * gamma + beta + post) over rows of width N (eps given).
+ * r row index = (row % r_mod) + r_off  (r_mod = rows for an ordinary residual; r_mod = T,
+ * r_off = 2 for the LearningPositionEmbedding table); post (or NULL) is row-aligned with x;
+ * act: 0 = identity, 1 = ReLU (ResidualBlock, model/residual.py:31-38).
+ * Saves mean/rstd per row.                                                              */
+#define SCA_ACT_NONE 0
+#define SCA_ACT_RELU 1
+typedef struct {
+  const float* x;
+  const float* r; /* or NULL */
+  const float* gamma;
+  const float* beta;
+  const float* post; /* or NULL */
+  float* y;
+  float* mean;
+  float* rstd;
+  int act;
+} sca_ln_fwd_problem;
+
+typedef struct {
+  const float* dy;
+  const float* x;
+  const float* r;
+  const float* gamma;
+  const float* mean;
+  const float* rstd;
+  const float* y;  /* forward output, read when act == ReLU (gradient gate y > 0) */
+  int act;
+  float* dpost;  /* or NULL: receives the (gated) gradient of `post` */
+  float* dx;     /* gradient of (x + r); ACCUM adds into dx */
+  float* dgamma; /* [N] written */
+  float* dbeta;  /* [N] written */
+  float* partial; /* workspace [2 * nblk * N], nblk from sca_layernorm_bwd_blocks() */
+} sca_ln_bwd_problem;
+
+#define SCA_LN_MAX_PROBLEMS 8
+int sca_layernorm_fwd(int nprob, const sca_ln_fwd_problem* probs, int rows, int N, int r_mod, int r_off,
+                      float eps, void* stream);
+int sca_layernorm_bwd_blocks(int rows);
+int sca_layernorm_bwd(int nprob, const sca_ln_bwd_problem* probs, int rows, int N, int r_mod, int r_off,
+                      int accumulate, void* stream);
+
+/* MaxPool1d(kernel 2, stride 2) over the frame axis of (B, T, C) -> (B, T/2, C)
+ * (ResidualBlock downsample, model/residual.py:40-43).  Backward routes each gradient to
+ * the first maximal element of its pair (ties -> the earlier frame), like ATen.          */
+typedef struct {
+  const float* x;
+  float* y;  /* forward */
+  const float* dy;
+  float* dx; /* backward (fully written, odd trailing frame gets 0) */
+} sca_pool_problem;
+#define SCA_POOL_MAX_PROBLEMS 8
+int sca_maxpool_t_fwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream);
+int sca_maxpool_t_bwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream);
+
+/* out[i, j] (+)= scale * sum_{s < S} in[s * stride_s + i * stride_i + j],  i < I, j < N.
+ * Column sums (bias gradients), slab reductions, position-table gradients.            */
+typedef struct {
+  const float* in;
+  float* out;
+  float scale;
+} sca_reduce_problem;
+
+#define SCA_REDUCE_MAX_PROBLEMS 16
+int sca_reduce_rows(int nprob, const sca_reduce_problem* probs, int S, int I, int N, long stride_s,
+                    long stride_i, int accumulate, void* stream);
+
+/* Coordinate mapping of one stream (fused A1+A2): keypoints (B*T, K_all, 2) fp32,
+ * joint index list idx[K] (int32, device) ->
+ *   xe[row, n] = sum_k kp[row, idx[k], 0] * Wx[n, k] + bx[n]
+ *   ye[row, n] = sum_k kp[row, idx[k], 1] * Wy[n, k] + by[n]                           */
+typedef struct {
+  const float* kp;
+  const int* idx;
+  int K;
+  const float* wx;
+  const float* bx;
+  const float* wy;
+  const float* by;
+  float* xe;
+  float* ye;
+} sca_coord_map_problem;
+
+typedef struct {
+  const float* kp;
+  const int* idx;
+  int K;
+  const float* wx;
+  const float* wy;
+  const float* dxe;
+  const float* dye;
+  float* dwx;     /* [N, K] written */
+  float* dwy;     /* [N, K] written */
+  float* dkp;     /* [rows, K_all, 2] accumulated into (must be zeroed by caller) or NULL */
+  float* partial; /* workspace [2 * nchunk * N * K], nchunk = sca_coord_map_bwd_chunks(rows) */
+} sca_coord_map_bwd_problem;
+
+#define SCA_MAP_MAX_PROBLEMS 8
+int sca_coord_map_fwd(int nprob, const sca_coord_map_problem* probs, int rows, int K_all, int N,
+                      void* stream);
+int sca_coord_map_bwd_chunks(int rows);
+int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* probs, int rows, int K_all, int N,
+                      void* stream);
+
+const char* sca_last_error(void);
+int sca_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCATTEN_H */

@@ -1,0 +1,140 @@
+"""ctypes binding of libscatten_hip.so (the C ABI declared in include/scatten.h).
+
+The product path has exactly one implementation: the HIP kernels in this library.  If the
+library is missing, or a tensor is not on a ROCm device, every op raises — there is no CPU
+fallback.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libscatten_hip.so")
+
+c_int, c_float, c_long, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_long, ctypes.c_void_p
+
+GEMM_NT, GEMM_NN, GEMM_TN = 0, 1, 2
+EPI_GELU, EPI_DGELU, EPI_ACCUM = 1, 2, 4
+GEMM_MAX_PROBLEMS = 12
+ATTN_MAX_PROBLEMS = 8
+LN_MAX_PROBLEMS = 8
+REDUCE_MAX_PROBLEMS = 16
+MAP_MAX_PROBLEMS = 8
+POOL_MAX_PROBLEMS = 8
+ACT_NONE, ACT_RELU = 0, 1
+
+
+class GemmSeg(ctypes.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("lda", c_int), ("ldb", c_int), ("K", c_int), ("alpha", c_float)]
+
+
+class GemmProblem(ctypes.Structure):
+    _fields_ = [("seg", GemmSeg * 3), ("nseg", c_int), ("M", c_int), ("N", c_int), ("C", c_void_p), ("ldc", c_int),
+                ("epi", c_int), ("bias", c_void_p), ("post_scale", c_float), ("resid", c_void_p), ("ldr", c_int),
+                ("aux", c_void_p), ("ldx", c_int), ("aux_out", c_void_p), ("ldo", c_int)]
+
+
+class AttnFwdProblem(ctypes.Structure):
+    _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("stat_m", c_void_p),
+                ("stat_ll", c_void_p), ("key_valid", c_void_p), ("add_mask", c_void_p)]
+
+
+class AttnBwdProblem(ctypes.Structure):
+    _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("dout", c_void_p),
+                ("stat_m", c_void_p), ("stat_ll", c_void_p), ("key_valid", c_void_p), ("add_mask", c_void_p),
+                ("dq", c_void_p), ("dk", c_void_p), ("dv", c_void_p), ("delta", c_void_p), ("dq_scale", c_float),
+                ("dv_scale", c_float)]
+
+
+class LnFwdProblem(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("r", c_void_p), ("gamma", c_void_p), ("beta", c_void_p), ("post", c_void_p),
+                ("y", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("act", c_int)]
+
+
+class LnBwdProblem(ctypes.Structure):
+    _fields_ = [("dy", c_void_p), ("x", c_void_p), ("r", c_void_p), ("gamma", c_void_p), ("mean", c_void_p),
+                ("rstd", c_void_p), ("y", c_void_p), ("act", c_int), ("dpost", c_void_p), ("dx", c_void_p),
+                ("dgamma", c_void_p), ("dbeta", c_void_p), ("partial", c_void_p)]
+
+
+class PoolProblem(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("dy", c_void_p), ("dx", c_void_p)]
+
+
+class ReduceProblem(ctypes.Structure):
+    _fields_ = [("inp", c_void_p), ("out", c_void_p), ("scale", c_float)]
+
+
+class CoordMapProblem(ctypes.Structure):
+    _fields_ = [("kp", c_void_p), ("idx", c_void_p), ("K", c_int), ("wx", c_void_p), ("bx", c_void_p),
+                ("wy", c_void_p), ("by", c_void_p), ("xe", c_void_p), ("ye", c_void_p)]
+
+
+class CoordMapBwdProblem(ctypes.Structure):
+    _fields_ = [("kp", c_void_p), ("idx", c_void_p), ("K", c_int), ("wx", c_void_p), ("wy", c_void_p),
+                ("dxe", c_void_p), ("dye", c_void_p), ("dwx", c_void_p), ("dwy", c_void_p), ("dkp", c_void_p),
+                ("partial", c_void_p)]
+
+
+EXPORTS = {
+    "sca_gemm": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
+    "sca_attn_bwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
+    "sca_layernorm_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p], c_int),
+    "sca_layernorm_bwd_blocks": ([c_int], c_int),
+    "sca_layernorm_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_maxpool_t_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_maxpool_t_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_reduce_rows": ([c_int, c_void_p, c_int, c_int, c_int, c_long, c_long, c_int, c_void_p], c_int),
+    "sca_coord_map_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_coord_map_bwd_chunks": ([c_int], c_int),
+    "sca_coord_map_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_last_error": ([], ctypes.c_char_p),
+    "sca_version": ([], c_int),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (once).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"scattennet_amd: {LIB_PATH} is missing — run __graft_entry__.build() "
+                               "(make -C scattennet_amd/csrc).  There is no fallback path.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (argt, rest) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        _lib = L
+    return _lib
+
+
+class HipOpError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().sca_last_error().decode()
+        if rc == 1:
+            raise ValueError(f"{what}: {msg}")
+        raise HipOpError(f"{what} failed ({rc}): {msg}")
+
+
+def stream_handle():
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32):
+            raise RuntimeError("scattennet_amd ops run only on ROCm (MI355X) fp32 tensors; got "
+                               f"{t.device} {t.dtype}.  There is no CPU fallback.")

@@ -1,0 +1,136 @@
+"""Drop-in attention operators (model/attention.py of tinh2044/SCAttenNet), MI355X-native.
+
+Same constructors, forward signatures, error behaviour and state_dict keys as the reference;
+the forward/backward run the grouped HIP kernels of `ops.py` (no ATen math on the path).
+
+`attention_mask` may be
+  * a `KeyPaddingMask` (what this package's SCA passes): per-clip key validity, the kernel
+    synthesises the additive mask of model/utils.py:3-28 in registers (fast path), or
+  * the reference's materialised additive (B, 1, Tq, Tk) fp32 tensor (general path: the
+    kernel adds it exactly as `attn_weights += attention_mask` does, attention.py:65/117/171).
+"""
+import torch
+from torch import nn
+
+from . import ops
+
+
+class BaseAttention(nn.Module):
+    """model/attention.py:8-26."""
+
+    def __init__(self, d_model, num_heads, dropout=0.0, bias=True):
+        super().__init__()
+        self.d_model = d_model
+        self.num_heads = num_heads
+        self.dropout = dropout
+        self.head_dim = d_model // num_heads
+        if (self.head_dim * num_heads) != self.d_model:
+            raise ValueError(
+                f"d_model must be divisible by num_heads (got `d_model`: {self.d_model}"
+                f" and `num_heads`: {num_heads})."
+            )
+        self.scaling = self.head_dim ** -0.5
+        # same construction order as the reference (k, v, q, out), so that a given torch
+        # seed produces the same initial weights
+        self.k_proj = nn.Linear(d_model, d_model, bias=bias)
+        self.v_proj = nn.Linear(d_model, d_model, bias=bias)
+        self.q_proj = nn.Linear(d_model, d_model, bias=bias)
+        self.out_proj = nn.Linear(d_model, d_model, bias=bias)
+
+    def _reinit_projections(self, d_model, bias):
+        # the subclasses re-create the four projections (attention.py:41-44/:91-95/:143-146);
+        # replicated for RNG-identical initialisation
+        self.q_proj = nn.Linear(d_model, d_model, bias=bias)
+        self.k_proj = nn.Linear(d_model, d_model, bias=bias)
+        self.v_proj = nn.Linear(d_model, d_model, bias=bias)
+        self.out_proj = nn.Linear(d_model, d_model, bias=bias)
+
+    def qkv_params(self):
+        return [self.q_proj.weight, self.q_proj.bias, self.k_proj.weight, self.k_proj.bias,
+                self.v_proj.weight, self.v_proj.bias]
+
+
+def _resolve_mask(mask, causal):
+    """-> (key_valid, add_mask, plus_one)."""
+    if mask is None:
+        return None, None, False
+    if isinstance(mask, ops.KeyPaddingMask):
+        return mask.key_valid, None, bool(causal and mask.causal_plus_one)
+    if torch.is_tensor(mask):
+        m = mask
+        if m.dim() == 4:
+            if m.shape[1] != 1:
+                raise ValueError("attention_mask must be (B, 1, Tq, Tk)")
+            m = m[:, 0]
+        return None, m.to(torch.float32).contiguous(), False
+    raise TypeError(f"unsupported attention_mask type {type(mask)}")
+
+
+def attention_grouped(attns, kind, hidden, kv, mask, resid=None):
+    """Run G attention operators of the same shape in lock-step (one launch per stage).
+
+    kind: "self" | "causal" | "cross".  Returns out_proj(attn) (+ resid when given, the
+    post-LN residual of the enclosing block fused into the out-projection epilogue)."""
+    G = len(attns)
+    a0 = attns[0]
+    for a in attns:
+        if a.training and a.dropout > 0:
+            raise NotImplementedError("attention dropout > 0 in training mode is not implemented")
+    params = []
+    for a in attns:
+        params += a.qkv_params()
+    if kind == "cross":
+        qkv = ops.QKVProjection.apply(G, True, a0.scaling, *hidden, *kv, *params)
+    else:
+        qkv = ops.QKVProjection.apply(G, False, a0.scaling, *hidden, *params)
+    q, k, v = qkv[0::3], qkv[1::3], qkv[2::3]
+    causal = kind == "causal"
+    key_valid, add_mask, plus_one = _resolve_mask(mask, causal)
+    o = ops.AttentionCore.apply(G, a0.num_heads, causal, plus_one, key_valid, add_mask, *q, *k, *v)
+    Wo = [a.out_proj.weight for a in attns]
+    bo = [a.out_proj.bias for a in attns]
+    if resid is None:
+        return list(ops.LinearResidual.apply(G, False, *o, *Wo, *bo))
+    return list(ops.LinearResidual.apply(G, True, *o, *Wo, *bo, *resid))
+
+
+class SelfAttention(BaseAttention):
+    """model/attention.py:29-76 — unmasked-in-time self-attention over the x-coordinate stream."""
+
+    def __init__(self, d_model, num_heads, dropout=0.0, bias=True):
+        super().__init__(d_model, num_heads, dropout=0.0, bias=True)
+        self.dropout = dropout
+        if (self.head_dim * num_heads) != d_model:
+            raise ValueError("d_model must be divisible by num_heads")
+        self._reinit_projections(d_model, bias)
+
+    def forward(self, hidden_states, attention_mask):
+        return attention_grouped([self], "self", [hidden_states], None, attention_mask)[0]
+
+
+class CrossAttention(BaseAttention):
+    """model/attention.py:79-128 — q from hidden_states, k/v from key_value_states (v from kv/2)."""
+
+    def __init__(self, d_model, num_heads, dropout=0.0, bias=True):
+        super().__init__(d_model, num_heads, dropout=0.0, bias=True)
+        self.dropout = dropout
+        if (self.head_dim * num_heads) != d_model:
+            raise ValueError("d_model must be divisible by num_heads")
+        self._reinit_projections(d_model, bias)
+
+    def forward(self, hidden_states, key_value_states, attention_mask):
+        return attention_grouped([self], "cross", [hidden_states], [key_value_states], attention_mask)[0]
+
+
+class SelfCausalAttention(BaseAttention):
+    """model/attention.py:131-182 — causal self-attention over the y-coordinate stream."""
+
+    def __init__(self, d_model, num_heads, dropout=0.0, bias=True):
+        super().__init__(d_model, num_heads, dropout=0.0, bias=True)
+        self.dropout = dropout
+        if (self.head_dim * num_heads) != d_model:
+            raise ValueError("d_model must be divisible by num_heads")
+        self._reinit_projections(d_model, bias)
+
+    def forward(self, hidden_states, attention_mask):
+        return attention_grouped([self], "causal", [hidden_states], None, attention_mask)[0]

@@ -1,0 +1,501 @@
+// Row-wise HBM-bound kernels of the SCA hot path:
+//   * residual-add + LayerNorm forward/backward (post-LN blocks, keypoint_module.py:67-72,
+//     :101-111) and position-embedding-add + LayerNorm (layers.py:15-30 + :161-162)
+//   * fixed-order row reductions (bias / LN-affine / position-table gradients)
+//   * fused stream slicing + de-interleave + CoordinateMapping forward/backward
+//     (model/__init__.py:133-142, keypoint_module.py:22-26, layers.py:111-123)
+// One wave per row for the LayerNorms (a 256-wide fp32 row = one float4 per lane).
+#include "common.h"
+#include "../../include/scatten.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------ LayerNorm
+struct LnFwdArgs {
+  sca_ln_fwd_problem p[SCA_LN_MAX_PROBLEMS];
+  int rows, N, r_mod, r_off;
+  float eps;
+};
+struct LnBwdArgs {
+  sca_ln_bwd_problem p[SCA_LN_MAX_PROBLEMS];
+  int rows, N, r_mod, r_off, accumulate, nblk;
+};
+
+constexpr int LN_MAXV = 16;  // values per lane -> N <= 1024
+
+__device__ __forceinline__ long rrow(int row, int r_mod, int r_off) { return (long)(row % r_mod) + r_off; }
+
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const LnFwdArgs a) {
+  const sca_ln_fwd_problem& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int N = a.N;
+  const float* xr = P.x + (long)row * N;
+  const float* rr = P.r ? P.r + rrow(row, a.r_mod, a.r_off) * N : nullptr;
+  float v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < LN_MAXV; ++j) {
+    const int c = lane + 64 * j;
+    float t = 0.f;
+    if (c < N) {
+      t = xr[c];
+      if (rr) t += rr[c];
+    }
+    v[j] = t;
+    s += t;
+  }
+  const float mean = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < LN_MAXV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < N) {
+      const float d = v[j] - mean;
+      q += d * d;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / N + a.eps);
+  float* yr = P.y + (long)row * N;
+  const float* pr = P.post ? P.post + (long)row * N : nullptr;
+#pragma unroll
+  for (int j = 0; j < LN_MAXV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < N) {
+      float o = (v[j] - mean) * rstd * P.gamma[c] + P.beta[c];
+      if (pr) o += pr[c];
+      if (P.act == SCA_ACT_RELU) o = fmaxf(o, 0.f);
+      yr[c] = o;
+    }
+  }
+  if (lane == 0) {
+    P.mean[row] = mean;
+    P.rstd[row] = rstd;
+  }
+}
+
+constexpr int LN_BWD_ROWS = 32;  // rows per workgroup (8 per wave)
+
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const LnBwdArgs a) {
+  const sca_ln_bwd_problem& P = a.p[blockIdx.y];
+  __shared__ float red[2][4][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int N = a.N;
+  float pg[LN_MAXV], pb[LN_MAXV];
+#pragma unroll
+  for (int j = 0; j < LN_MAXV; ++j) pg[j] = pb[j] = 0.f;
+  const int rbeg = blockIdx.x * LN_BWD_ROWS;
+  for (int i = w; i < LN_BWD_ROWS; i += 4) {
+    const int row = rbeg + i;
+    if (row >= a.rows) break;
+    const float mean = P.mean[row], rstd = P.rstd[row];
+    const float* xr = P.x + (long)row * N;
+    const float* rr = P.r ? P.r + rrow(row, a.r_mod, a.r_off) * N : nullptr;
+    const float* dyr = P.dy + (long)row * N;
+    const float* yr = P.act ? P.y + (long)row * N : nullptr;
+    float* dpr = P.dpost ? P.dpost + (long)row * N : nullptr;
+    float xh[LN_MAXV], g[LN_MAXV];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < LN_MAXV; ++j) {
+      const int c = lane + 64 * j;
+      xh[j] = g[j] = 0.f;
+      if (c < N) {
+        float t = xr[c];
+        if (rr) t += rr[c];
+        float dy = dyr[c];
+        if (yr && !(yr[c] > 0.f)) dy = 0.f;  // ReLU gate (threshold_backward: out > 0)
+        if (dpr) dpr[c] = dy;
+        xh[j] = (t - mean) * rstd;
+        g[j] = dy * P.gamma[c];
+        sg += g[j];
+        sgx += g[j] * xh[j];
+        pg[j] += dy * xh[j];
+        pb[j] += dy;
+      }
+    }
+    const float mg = wave_sum(sg) / N, mgx = wave_sum(sgx) / N;
+    float* dxr = P.dx + (long)row * N;
+#pragma unroll
+    for (int j = 0; j < LN_MAXV; ++j) {
+      const int c = lane + 64 * j;
+      if (c < N) {
+        float d = rstd * (g[j] - mg - xh[j] * mgx);
+        if (a.accumulate) d += dxr[c];
+        dxr[c] = d;
+      }
+    }
+  }
+  // combine the 4 waves' partials in fixed order, one partial row per workgroup
+#pragma unroll
+  for (int j = 0; j < LN_MAXV; ++j) {
+    const int c = lane + 64 * j;
+    if (c < N) {
+      red[0][w][c] = pg[j];
+      red[1][w][c] = pb[j];
+    }
+  }
+  __syncthreads();
+  float* part = P.partial;
+  for (int c = threadIdx.x; c < N; c += 256) {
+    const float gsum = ((red[0][0][c] + red[0][1][c]) + red[0][2][c]) + red[0][3][c];
+    const float bsum = ((red[1][0][c] + red[1][1][c]) + red[1][2][c]) + red[1][3][c];
+    part[(long)blockIdx.x * N + c] = gsum;
+    part[((long)a.nblk + blockIdx.x) * N + c] = bsum;
+  }
+}
+
+// ------------------------------------------------------------------------------ reductions
+struct ReduceArgs {
+  sca_reduce_problem p[SCA_REDUCE_MAX_PROBLEMS];
+  int S, I, N, accumulate;
+  long stride_s, stride_i;
+};
+
+// grid (ceil(N/64), I, nprob), 512 threads: wave w sums s = w, w+8, ...; fixed-order combine.
+__global__ __launch_bounds__(512) void reduce_rows_kernel(const ReduceArgs a) {
+  const sca_reduce_problem& P = a.p[blockIdx.z];
+  __shared__ float red[8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const int i = blockIdx.y;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < a.N) {
+    const float* base = P.in + (long)i * a.stride_i + j;
+    int s = w;
+    for (; s + 24 < a.S; s += 32) {
+      s0 += base[(long)s * a.stride_s];
+      s1 += base[(long)(s + 8) * a.stride_s];
+      s2 += base[(long)(s + 16) * a.stride_s];
+      s3 += base[(long)(s + 24) * a.stride_s];
+    }
+    for (; s < a.S; s += 8) s0 += base[(long)s * a.stride_s];
+  }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && j < a.N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][lane];
+    t *= P.scale;
+    float* o = P.out + (long)i * a.N + j;
+    if (a.accumulate) t += *o;
+    *o = t;
+  }
+}
+
+int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
+  dim3 grid((a.N + 63) / 64, a.I, nprob);
+  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(512), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
+// ------------------------------------------------------------------------------ MaxPool1d(2,2) over T
+struct PoolArgs {
+  sca_pool_problem p[SCA_POOL_MAX_PROBLEMS];
+  int B, T, C;
+};
+
+__global__ __launch_bounds__(256) void maxpool_t_fwd_kernel(const PoolArgs a) {
+  const sca_pool_problem& P = a.p[blockIdx.y];
+  const int To = a.T / 2;
+  const long n = (long)a.B * To * a.C;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % a.C);
+    const long bt = e / a.C;
+    const int t = (int)(bt % To), b = (int)(bt / To);
+    const float* src = P.x + ((long)b * a.T + 2 * t) * a.C + c;
+    const float x0 = src[0], x1 = src[a.C];
+    P.y[e] = (x1 > x0) ? x1 : x0;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_t_bwd_kernel(const PoolArgs a) {
+  const sca_pool_problem& P = a.p[blockIdx.y];
+  const int To = a.T / 2;
+  const long n = (long)a.B * a.T * a.C;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % a.C);
+    const long bt = e / a.C;
+    const int t = (int)(bt % a.T), b = (int)(bt / a.T);
+    float g = 0.f;
+    const int to = t >> 1;
+    if (to < To) {
+      const float* src = P.x + ((long)b * a.T + 2 * to) * a.C + c;
+      const float x0 = src[0], x1 = src[a.C];
+      const bool second = x1 > x0;
+      if ((t & 1) == (second ? 1 : 0)) g = P.dy[((long)b * To + to) * a.C + c];
+    }
+    P.dx[e] = g;
+  }
+}
+
+// ------------------------------------------------------------------------------ coordinate mapping
+struct MapArgs {
+  sca_coord_map_problem p[SCA_MAP_MAX_PROBLEMS];
+  int rows, K_all, N;
+};
+struct MapBwdArgs {
+  sca_coord_map_bwd_problem p[SCA_MAP_MAX_PROBLEMS];
+  int rows, K_all, N, nchunk;
+};
+
+constexpr int MAP_ROWS = 16;   // rows per workgroup (forward)
+constexpr int MAP_KMAX = 136;  // max joints per stream (K=133 COCO-WholeBody face+body fits)
+constexpr int MAP_CHUNK = 32;  // rows per partial (backward)
+
+// Gather this workgroup's rows' joints into LDS: xs[r][k], ys[r][k].
+__device__ __forceinline__ void gather_coords(float (*xs)[MAP_KMAX], float (*ys)[MAP_KMAX], const float* kp,
+                                              const int* idx, int K, int K_all, int row0, int nrows, int rows) {
+  for (int e = threadIdx.x; e < nrows * K; e += blockDim.x) {
+    const int r = e / K, k = e % K;
+    const int row = row0 + r;
+    float x = 0.f, y = 0.f;
+    if (row < rows) {
+      const float* src = kp + ((long)row * K_all + idx[k]) * 2;
+      x = src[0];
+      y = src[1];
+    }
+    xs[r][k] = x;
+    ys[r][k] = y;
+  }
+}
+
+__global__ __launch_bounds__(256) void coord_map_fwd_kernel(const MapArgs a) {
+  const sca_coord_map_problem& P = a.p[blockIdx.y];
+  __shared__ float xs[MAP_ROWS][MAP_KMAX], ys[MAP_ROWS][MAP_KMAX];
+  const int row0 = blockIdx.x * MAP_ROWS;
+  const int K = P.K;
+  gather_coords(xs, ys, P.kp, P.idx, K, a.K_all, row0, MAP_ROWS, a.rows);
+  __syncthreads();
+  for (int n = threadIdx.x; n < a.N; n += 256) {
+    float ax[MAP_ROWS], ay[MAP_ROWS];
+#pragma unroll
+    for (int r = 0; r < MAP_ROWS; ++r) ax[r] = ay[r] = 0.f;
+    const float* wxr = P.wx + (long)n * K;
+    const float* wyr = P.wy + (long)n * K;
+    for (int k = 0; k < K; ++k) {
+      const float wx = wxr[k], wy = wyr[k];
+#pragma unroll
+      for (int r = 0; r < MAP_ROWS; ++r) {
+        ax[r] = fmaf(xs[r][k], wx, ax[r]);
+        ay[r] = fmaf(ys[r][k], wy, ay[r]);
+      }
+    }
+    const float bx = P.bx ? P.bx[n] : 0.f, by = P.by ? P.by[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < MAP_ROWS; ++r) {
+      const int row = row0 + r;
+      if (row < a.rows) {
+        P.xe[(long)row * a.N + n] = ax[r] + bx;
+        P.ye[(long)row * a.N + n] = ay[r] + by;
+      }
+    }
+  }
+}
+
+// Partial weight gradients: partial[c][chunk][n][k] = sum_{rows in chunk} d{x,y}e[row][n] * {x,y}[row][k]
+__global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a) {
+  const sca_coord_map_bwd_problem& P = a.p[blockIdx.y];
+  __shared__ float xs[MAP_CHUNK][MAP_KMAX], ys[MAP_CHUNK][MAP_KMAX];
+  const int row0 = blockIdx.x * MAP_CHUNK;
+  const int K = P.K;
+  const int nr = min(MAP_CHUNK, a.rows - row0);
+  gather_coords(xs, ys, P.kp, P.idx, K, a.K_all, row0, MAP_CHUNK, a.rows);
+  __syncthreads();
+  constexpr int KC = 16;
+  for (int n = threadIdx.x; n < a.N; n += 256) {
+    for (int kc = 0; kc < K; kc += KC) {
+      float gx[KC], gy[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) gx[j] = gy[j] = 0.f;
+      for (int r = 0; r < nr; ++r) {
+        const float dx = P.dxe[(long)(row0 + r) * a.N + n];
+        const float dy = P.dye[(long)(row0 + r) * a.N + n];
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+          if (kc + j < K) {
+            gx[j] = fmaf(dx, xs[r][kc + j], gx[j]);
+            gy[j] = fmaf(dy, ys[r][kc + j], gy[j]);
+          }
+        }
+      }
+      float* px = P.partial + ((long)blockIdx.x * a.N + n) * K;
+      float* py = P.partial + ((long)(a.nchunk + blockIdx.x) * a.N + n) * K;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        if (kc + j < K) {
+          px[kc + j] = gx[j];
+          py[kc + j] = gy[j];
+        }
+      }
+    }
+  }
+}
+
+// Keypoint gradients (only when the keypoints require grad): one wave per row.
+__global__ __launch_bounds__(256) void coord_map_bwd_kp_kernel(const MapBwdArgs a) {
+  const sca_coord_map_bwd_problem& P = a.p[blockIdx.y];
+  if (!P.dkp) return;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const float* dxr = P.dxe + (long)row * a.N;
+  const float* dyr = P.dye + (long)row * a.N;
+  for (int k = lane; k < P.K; k += 64) {
+    float sx = 0.f, sy = 0.f;
+    for (int n = 0; n < a.N; ++n) {
+      sx = fmaf(dxr[n], P.wx[(long)n * P.K + k], sx);
+      sy = fmaf(dyr[n], P.wy[(long)n * P.K + k], sy);
+    }
+    float* dst = P.dkp + ((long)row * a.K_all + P.idx[k]) * 2;
+    atomicAdd(dst, sx);
+    atomicAdd(dst + 1, sy);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ C ABI
+extern "C" void sca_set_error(const char* msg);
+
+extern "C" int sca_layernorm_fwd(int nprob, const sca_ln_fwd_problem* probs, int rows, int N, int r_mod,
+                                 int r_off, float eps, void* stream) {
+  if (nprob < 1 || nprob > SCA_LN_MAX_PROBLEMS || N < 1 || N > 64 * LN_MAXV || rows < 0 || r_mod < 1) {
+    sca_set_error("sca_layernorm_fwd: bad arguments (N must be <= 1024)");
+    return SCA_ERR_ARG;
+  }
+  if (rows == 0) return SCA_OK;
+  LnFwdArgs a;
+  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  a.rows = rows; a.N = N; a.r_mod = r_mod; a.r_off = r_off; a.eps = eps;
+  dim3 grid((rows + 3) / 4, nprob);
+  hipLaunchKernelGGL(ln_fwd_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_layernorm_fwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_maxpool_t_fwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream) {
+  if (nprob < 1 || nprob > SCA_POOL_MAX_PROBLEMS || B < 0 || T < 0 || C < 1) {
+    sca_set_error("sca_maxpool_t_fwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  PoolArgs a;
+  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  a.B = B; a.T = T; a.C = C;
+  const long n = (long)B * (T / 2) * C;
+  if (n == 0) return SCA_OK;
+  const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(maxpool_t_fwd_kernel, dim3(blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_maxpool_t_fwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_maxpool_t_bwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream) {
+  if (nprob < 1 || nprob > SCA_POOL_MAX_PROBLEMS || B < 0 || T < 0 || C < 1) {
+    sca_set_error("sca_maxpool_t_bwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  PoolArgs a;
+  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  a.B = B; a.T = T; a.C = C;
+  const long n = (long)B * T * C;
+  if (n == 0) return SCA_OK;
+  const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(maxpool_t_bwd_kernel, dim3(blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_maxpool_t_bwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_layernorm_bwd_blocks(int rows) { return (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS; }
+
+extern "C" int sca_layernorm_bwd(int nprob, const sca_ln_bwd_problem* probs, int rows, int N, int r_mod,
+                                 int r_off, int accumulate, void* stream) {
+  if (nprob < 1 || nprob > SCA_LN_MAX_PROBLEMS || N < 1 || N > 64 * LN_MAXV || rows < 1 || r_mod < 1) {
+    sca_set_error("sca_layernorm_bwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  LnBwdArgs a;
+  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  a.rows = rows; a.N = N; a.r_mod = r_mod; a.r_off = r_off; a.accumulate = accumulate;
+  a.nblk = sca_layernorm_bwd_blocks(rows);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(a.nblk, nprob), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_layernorm_bwd: launch failed"); return SCA_ERR_LAUNCH; }
+  // dgamma / dbeta = fixed-order sums of the per-workgroup partial rows
+  ReduceArgs r;
+  int np = 0;
+  for (int i = 0; i < nprob; ++i) {
+    r.p[np++] = sca_reduce_problem{probs[i].partial, probs[i].dgamma, 1.0f};
+    r.p[np++] = sca_reduce_problem{probs[i].partial + (long)a.nblk * N, probs[i].dbeta, 1.0f};
+  }
+  r.S = a.nblk; r.I = 1; r.N = N; r.accumulate = 0; r.stride_s = N; r.stride_i = 0;
+  if (launch_reduce(r, np, st) != SCA_OK) { sca_set_error("sca_layernorm_bwd: reduce launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_reduce_rows(int nprob, const sca_reduce_problem* probs, int S, int I, int N, long stride_s,
+                               long stride_i, int accumulate, void* stream) {
+  if (nprob < 1 || nprob > SCA_REDUCE_MAX_PROBLEMS || S < 0 || I < 1 || N < 1) {
+    sca_set_error("sca_reduce_rows: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  ReduceArgs r;
+  for (int i = 0; i < nprob; ++i) r.p[i] = probs[i];
+  r.S = S; r.I = I; r.N = N; r.accumulate = accumulate; r.stride_s = stride_s; r.stride_i = stride_i;
+  if (launch_reduce(r, nprob, reinterpret_cast<hipStream_t>(stream)) != SCA_OK) {
+    sca_set_error("sca_reduce_rows: launch failed");
+    return SCA_ERR_LAUNCH;
+  }
+  return SCA_OK;
+}
+
+extern "C" int sca_coord_map_fwd(int nprob, const sca_coord_map_problem* probs, int rows, int K_all, int N,
+                                 void* stream) {
+  if (nprob < 1 || nprob > SCA_MAP_MAX_PROBLEMS || rows < 0 || N < 1) {
+    sca_set_error("sca_coord_map_fwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  MapArgs a;
+  for (int i = 0; i < nprob; ++i) {
+    if (probs[i].K < 1 || probs[i].K > MAP_KMAX) { sca_set_error("sca_coord_map_fwd: K must be 1..136"); return SCA_ERR_ARG; }
+    a.p[i] = probs[i];
+  }
+  if (rows == 0) return SCA_OK;
+  a.rows = rows; a.K_all = K_all; a.N = N;
+  dim3 grid((rows + MAP_ROWS - 1) / MAP_ROWS, nprob);
+  hipLaunchKernelGGL(coord_map_fwd_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_coord_map_fwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_coord_map_bwd_chunks(int rows) { return (rows + MAP_CHUNK - 1) / MAP_CHUNK; }
+
+extern "C" int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* probs, int rows, int K_all, int N,
+                                 void* stream) {
+  if (nprob < 1 || nprob > SCA_MAP_MAX_PROBLEMS || rows < 1 || N < 1) {
+    sca_set_error("sca_coord_map_bwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  MapBwdArgs a;
+  for (int i = 0; i < nprob; ++i) {
+    if (probs[i].K < 1 || probs[i].K > MAP_KMAX) { sca_set_error("sca_coord_map_bwd: K must be 1..136"); return SCA_ERR_ARG; }
+    a.p[i] = probs[i];
+  }
+  a.rows = rows; a.K_all = K_all; a.N = N; a.nchunk = sca_coord_map_bwd_chunks(rows);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(coord_map_bwd_w_kernel, dim3(a.nchunk, nprob), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(coord_map_bwd_kp_kernel, dim3((rows + 3) / 4, nprob), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_coord_map_bwd: launch failed"); return SCA_ERR_LAUNCH; }
+  // dW = fixed-order sum over row chunks (problems may differ in K: one reduce each)
+  for (int i = 0; i < nprob; ++i) {
+    const int NK = N * probs[i].K;
+    ReduceArgs r;
+    r.p[0] = sca_reduce_problem{probs[i].partial, probs[i].dwx, 1.0f};
+    r.p[1] = sca_reduce_problem{probs[i].partial + (long)a.nchunk * NK, probs[i].dwy, 1.0f};
+    r.S = a.nchunk; r.I = 1; r.N = NK; r.accumulate = 0; r.stride_s = NK; r.stride_i = 0;
+    if (launch_reduce(r, 2, st) != SCA_OK) { sca_set_error("sca_coord_map_bwd: reduce launch failed"); return SCA_ERR_LAUNCH; }
+  }
+  return SCA_OK;
+}

@@ -1,0 +1,181 @@
+"""Drop-in SCA blocks of model/keypoint_module.py (tinh2044/SCAttenNet), MI355X-native.
+
+Each module keeps the reference constructor, forward signature and state_dict keys.  The
+math lives in `*_grouped` functions that run G same-shaped modules (one per keypoint
+stream) in lock-step, one HIP launch per stage for all streams; a module's own `forward` is
+the G = 1 case.  `KeypointStreams` drives several KeypointModules that way.
+"""
+import torch
+from torch import nn
+
+from . import ops
+from .attention import CrossAttention, SelfAttention, SelfCausalAttention, attention_grouped
+from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, check_dropout,
+                     coordinate_mapping_grouped, ffn_grouped, layernorm_grouped, pos_embed_layernorm_grouped)
+from .residual import ResidualNetwork, residual_network_grouped
+from .utils import key_padding_mask
+
+
+# --------------------------------------------------------------------------- A9
+class CoordinateAttention(nn.Module):
+    """model/keypoint_module.py:34-80 — post-LN attention block; "causal_attn" has no MLP."""
+
+    def __init__(self, cfg, attn_type="self_attn"):
+        super().__init__()
+        self.attn_type = attn_type
+        if attn_type == "self_attn":
+            self.attn = SelfAttention(d_model=cfg["d_model"], num_heads=cfg["attention_heads"],
+                                      dropout=cfg["attention_dropout"])
+            self.mlp = FeedForward(cfg["d_model"], cfg["ff_dim"], cfg["dropout"])
+            self.last_layer_norm = nn.LayerNorm(cfg["d_model"])
+        elif attn_type == "causal_attn":
+            self.attn = SelfCausalAttention(d_model=cfg["d_model"], num_heads=cfg["attention_heads"],
+                                            dropout=cfg["attention_dropout"])
+            self.mlp = nn.Identity()
+            self.last_layer_norm = nn.Identity()
+        else:
+            raise ValueError(f"Invalid attention type: {attn_type}")
+        self.attn_layer_norm = nn.LayerNorm(cfg["d_model"])
+        self.dropout = cfg["dropout"]
+        self.activation_fn = nn.GELU()
+
+    def forward(self, coord_embed, attention_mask=None):
+        return coordinate_attention_grouped([self], [coord_embed], attention_mask)[0]
+
+
+def coordinate_attention_grouped(blocks, xs, mask):
+    """h = LN(x + Attn(x)); self type: h = LN(h + FFN(h))  (keypoint_module.py:61-80).
+    The residual adds ride in the out-projection / fc2 epilogues."""
+    check_dropout(blocks)
+    kind = "self" if blocks[0].attn_type == "self_attn" else "causal"
+    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=xs)
+    h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
+    if kind == "self":
+        h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
+        h = layernorm_grouped([b.last_layer_norm for b in blocks], h)
+    return h
+
+
+# --------------------------------------------------------------------------- A10
+class CoordinatesMerge(nn.Module):
+    """model/keypoint_module.py:83-115 — y <- CrossAttn(q=y, kv=x) then FFN, both post-LN."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.attn = CrossAttention(d_model=cfg["d_model"], num_heads=cfg["attention_heads"],
+                                   dropout=cfg["attention_dropout"])
+        self.mlp = FeedForward(cfg["d_model"], cfg["ff_dim"], cfg["dropout"])
+        self.attn_layer_norm = nn.LayerNorm(cfg["d_model"])
+        self.last_layer_norm = nn.LayerNorm(cfg["d_model"])
+        self.dropout = cfg["dropout"]
+
+    def forward(self, y_embed, x_embed, cross_attn_mask=None):
+        return coordinates_merge_grouped([self], [y_embed], [x_embed], cross_attn_mask)[0]
+
+
+def coordinates_merge_grouped(blocks, ys, xs, mask):
+    check_dropout(blocks)
+    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=ys)
+    h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
+    h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
+    return layernorm_grouped([b.last_layer_norm for b in blocks], h)
+
+
+# --------------------------------------------------------------------------- A11
+class SeparativeCoordinateAttention(nn.Module):
+    """model/keypoint_module.py:118-198."""
+
+    def __init__(self, cfg=None):
+        super().__init__()
+        self.dropout = cfg["dropout"]
+        self.self_attn_layers = nn.ModuleList(
+            [CoordinateAttention(cfg, attn_type="self_attn") for _ in range(cfg["attn_layers"])])
+        self.causal_attn_layers = nn.ModuleList(
+            [CoordinateAttention(cfg, attn_type="causal_attn") for _ in range(cfg["attn_layers"])])
+        self.coordinates_merge = nn.ModuleList([CoordinatesMerge(cfg) for _ in range(cfg["attn_layers"])])
+        self.first_self_norm = nn.LayerNorm(cfg["d_model"])
+        self.first_causal_norm = nn.LayerNorm(cfg["d_model"])
+        self.self_pos_embed = LearningPositionEmbedding(cfg["max_position_embeddings"], cfg["d_model"])
+        self.causal_pos_embed = LearningPositionEmbedding(cfg["max_position_embeddings"], cfg["d_model"])
+        self.x_self = cfg.get("self_attn_x", True)
+
+    def forward(self, x_embed, y_embed, attention_mask=None, return_attn_map=False):
+        outs, s_maps = sca_grouped([self], [x_embed], [y_embed], attention_mask)
+        if return_attn_map:
+            return {"outputs": outs[0], "self_attn_map": s_maps[0], "causal_attn_map": outs[0]}
+        return outs[0]
+
+
+def sca_grouped(scas, xs, ys, attention_mask):
+    """Returns (y-stream outputs, final x-stream maps) for G same-shaped SCA stacks.
+
+    Data dependency (keypoint_module.py:176-187): every merge layer reads the FINAL x-stream
+    map, so the L self layers run first, then L x (causal, merge)."""
+    check_dropout(scas)
+    if attention_mask is None:
+        raise AttributeError("'NoneType' object has no attribute 'size'")  # reference: mask.size()
+    x_self = scas[0].x_self
+    se, ce = (xs, ys) if x_self else (ys, xs)
+    se = pos_embed_layernorm_grouped([m.self_pos_embed for m in scas], [m.first_self_norm for m in scas], se)
+    ce = pos_embed_layernorm_grouped([m.causal_pos_embed for m in scas], [m.first_causal_norm for m in scas], ce)
+    self_mask = key_padding_mask(attention_mask)  # model/utils.py:3-12
+    causal_mask = key_padding_mask(attention_mask, causal=True)  # model/utils.py:15-28
+    cross_mask = self_mask  # create_attention_mask(tgt_len=T) — same key padding
+    L = len(scas[0].self_attn_layers)
+    s = se
+    for i in range(L):
+        s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, self_mask)
+    c = ce
+    for i in range(L):
+        c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
+        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask)
+    return c, s
+
+
+# --------------------------------------------------------------------------- A1 + A2 + A11 + A12
+class KeypointModule(nn.Module):
+    """model/keypoint_module.py:13-31 — one anatomical stream: mapping -> SCA -> residual."""
+
+    def __init__(self, joint_idx, num_frame, cfg=None):
+        super().__init__()
+        self.joint_idx = joint_idx
+        self.num_frame = num_frame
+        self.coordinate_mapping = CoordinateMapping(len(joint_idx), cfg["d_model"])
+        self.sca = SeparativeCoordinateAttention(cfg)
+        self.residual = ResidualNetwork(cfg["residual_blocks"])
+
+    def forward(self, keypoints, attention_mask=None):
+        # `keypoints` is the stream's own (B, T, K, 2) slice, as MSCA_Net passes it
+        idx = self.coordinate_mapping.joint_index(keypoints.device)
+        xe, ye = coordinate_mapping_grouped([self.coordinate_mapping], keypoints, [idx])
+        out, _ = sca_grouped([self.sca], xe, ye, attention_mask)
+        return residual_network_grouped([self.residual], out)[0]
+
+
+class KeypointStreams(nn.Module):
+    """Several KeypointModules run in lock-step over ONE (B, T, K_all, 2) keypoint tensor.
+
+    The stream slicing of MSCA_Net.forward (model/__init__.py:133-142) is fused into the
+    mapping kernel's gather, and every later stage runs all streams in one launch.  Streams
+    must share d_model / heads / layers (they do: one cfg).  `with_residual=False` stops after
+    the SCA stack (BASELINE config 2); True adds the ResidualNetwork (config 3)."""
+
+    def __init__(self, modules, with_residual=True):
+        super().__init__()
+        self.streams = nn.ModuleList(modules)
+        self.with_residual = with_residual
+        self._idx = None
+
+    def joint_indices(self, device):
+        if self._idx is None or self._idx[0].device != device:
+            self._idx = [torch.tensor(list(m.joint_idx), dtype=torch.int32, device=device) for m in self.streams]
+        return self._idx
+
+    def forward(self, keypoints, attention_mask):
+        mods = list(self.streams)
+        xe, ye = coordinate_mapping_grouped([m.coordinate_mapping for m in mods], keypoints,
+                                            self.joint_indices(keypoints.device))
+        out, _ = sca_grouped([m.sca for m in mods], xe, ye, attention_mask)
+        if self.with_residual:
+            out = residual_network_grouped([m.residual for m in mods], out)
+        return out

@@ -1,0 +1,582 @@
+"""Grouped autograd ops of the SCA hot path, each forward/backward a launch of the HIP C ABI.
+
+Every op works on a GROUP of G independent problems (the keypoint streams of one clip batch,
+or G = 1 for a standalone module), so that one launch covers all streams: at the BASELINE
+config-2 shape (B=8, T=256, d=256) a single stream's GEMM is only 2048 x 256 x 256.
+
+Activations are contiguous (B, T, C) fp32 on the GPU, viewed as (M = B*T, C) row-major.
+Parameters keep the nn.Linear / nn.LayerNorm layouts of the reference (W is [out, in]).
+"""
+import torch
+from torch.autograd import Function
+
+from . import _lib as L
+from ._lib import ptr
+
+# --------------------------------------------------------------------------- launch profiling
+class LaunchProfiler:
+    """While active, every C-ABI call is bracketed by HIP events on the stream it launches
+    on, with its algorithmic FLOPs; used by bench.py for the dominant kernel's roofline."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _PROFILER
+        _PROFILER = self
+        return self
+
+    def __exit__(self, *exc):
+        global _PROFILER
+        _PROFILER = None
+
+    def stats(self):
+        out = {}
+        for key, flops, e0, e1 in self.records:
+            st = out.setdefault(key, {"flops": 0.0, "seconds": 0.0, "launches": 0})
+            st["flops"] += flops
+            st["seconds"] += e0.elapsed_time(e1) / 1e3
+            st["launches"] += 1
+        return out
+
+    def dominant(self):
+        st = self.stats()
+        k = max(st, key=lambda n: st[n]["seconds"])
+        return k, st[k]
+
+
+_PROFILER = None
+
+
+class _timed:
+    def __init__(self, key, flops):
+        self.key, self.flops = key, flops
+
+    def __enter__(self):
+        if _PROFILER is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _PROFILER is not None:
+            self.e1.record()
+            _PROFILER.records.append((self.key, self.flops, self.e0, self.e1))
+
+
+_GEMM_NAMES = {0: "gemm_kernel<NT,64,64>", 1: "gemm_kernel<NN,64,64>", 2: "gemm_kernel<TN,64,64>"}
+
+# --------------------------------------------------------------------------- launch helpers
+_NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0)
+
+
+def _seg(A, B, lda, ldb, K, alpha=1.0):
+    return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha)
+
+
+def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=0, aux=None, ldx=0,
+          aux_out=None, ldo=0):
+    s = list(segs) + [_NOSEG] * (3 - len(segs))
+    return L.GemmProblem((L.GemmSeg * 3)(*s), len(segs), M, N, C.data_ptr(), ldc, epi, ptr(bias), post_scale,
+                         ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo)
+
+
+def gemm(layout, probs, splitk=1, ws=None):
+    lib = L.lib()
+    st = L.stream_handle()
+    for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
+        chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
+        arr = (L.GemmProblem * len(chunk))(*chunk)
+        flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
+        with _timed(_GEMM_NAMES[layout], flops):
+            L.check(lib.sca_gemm(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm")
+
+
+def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
+    """pairs: list of (in_tensor, out_tensor_or_view, scale)."""
+    lib = L.lib()
+    st = L.stream_handle()
+    for i in range(0, len(pairs), L.REDUCE_MAX_PROBLEMS):
+        chunk = pairs[i:i + L.REDUCE_MAX_PROBLEMS]
+        arr = (L.ReduceProblem * len(chunk))(*[L.ReduceProblem(a.data_ptr(), o.data_ptr(), s) for a, o, s in chunk])
+        L.check(lib.sca_reduce_rows(len(chunk), arr, S, I, N, stride_s, stride_i, int(accumulate), st),
+                "sca_reduce_rows")
+
+
+def _splitk_for(M_red, n_out_tiles):
+    """Split the long reduction (rows of the batch) of weight-gradient GEMMs so that the
+    grid covers the 256 CUs about twice."""
+    sk = 1
+    while sk < 8 and n_out_tiles * sk < 512 and M_red // (sk * 2) >= 256:
+        sk *= 2
+    return sk
+
+
+def weight_grads(items, M=None):
+    """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = alpha_g * colsum(dY_g).
+
+    items: list of (dY[M,out], X[M,in], alpha, W_like, has_bias[, bias_scale]) -> [(dW, db)].
+    bias_scale defaults to alpha; it differs when alpha scales the INPUT X (v from kv/2:
+    dWv = dV^T (kv/2) but dbv = colsum(dV))."""
+    out = []
+    by_shape = {}  # split-K needs equal problem shapes within a launch
+    items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
+    for idx, (dY, X, alpha, W, has_bias, _) in enumerate(items):
+        n_out, n_in = W.shape
+        dW = torch.empty_like(W)
+        db = torch.empty(n_out, device=W.device, dtype=W.dtype) if has_bias else None
+        out.append((dW, db))
+        by_shape.setdefault((n_out, n_in, dY.shape[0]), []).append(idx)
+    for (n_out, n_in, Mr), idxs in by_shape.items():
+        tiles = ((n_out + 63) // 64) * ((n_in + 63) // 64) * len(idxs)
+        sk = _splitk_for(Mr, tiles)
+        for c in range(0, len(idxs), L.GEMM_MAX_PROBLEMS):
+            sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
+            probs = []
+            for i in sub:
+                dY, X, alpha, W, _, _ = items[i]
+                probs.append(_prob([_seg(dY, X, n_out, n_in, Mr, alpha)], out[i][0], n_out, n_in, n_in))
+            ws = None
+            if sk > 1:
+                ws = torch.empty(len(sub) * sk * n_out * n_in, device=items[0][0].device, dtype=torch.float32)
+            gemm(L.GEMM_TN, probs, splitk=sk, ws=ws)
+    by_w = {}  # bias grads, grouped by (width, rows)
+    for i, (dY, _, _, _, _, bscale) in enumerate(items):
+        if out[i][1] is not None:
+            by_w.setdefault((dY.shape[1], dY.shape[0]), []).append((dY, out[i][1], bscale))
+    for (w, Mr), ps in by_w.items():
+        reduce_rows(ps, Mr, 1, w, w, 0)
+    return out
+
+
+def _flat(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+def _contig(ts):
+    return [t if t is None or t.is_contiguous() else t.contiguous() for t in ts]
+
+
+def _zeros_for_none(grads, refs):
+    return [g if g is not None else torch.zeros_like(r) for g, r in zip(grads, refs)]
+
+
+# --------------------------------------------------------------------------- q/k/v projections
+class QKVProjection(Function):
+    """q = (x_q Wq^T + bq) * scale ; k = x_kv Wk^T + bk ; v = (alpha_v * x_kv) Wv^T + bv.
+
+    self/causal attention: x_kv is x_q (attention.py:49-51, :151-153);
+    cross attention: x_q = hidden_states, x_kv = key_value_states, alpha_v = 0.5 (:101-103)."""
+
+    @staticmethod
+    def forward(ctx, G, cross, scale, *ts):
+        xq = _contig(ts[:G])
+        xkv = _contig(ts[G:2 * G]) if cross else xq
+        W = ts[2 * G:] if cross else ts[G:]
+        L.require_device(*xq, *xkv)
+        B, T, d = xq[0].shape
+        Tk = xkv[0].shape[1]
+        alpha_v = 0.5 if cross else 1.0
+        outs = []
+        probs = []
+        for g in range(G):
+            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
+            xf, kf = _flat(xq[g]), _flat(xkv[g])
+            q = xq[g].new_empty(B, T, d)
+            k = xq[g].new_empty(B, Tk, d)
+            v = xq[g].new_empty(B, Tk, d)
+            probs.append(_prob([_seg(xf, Wq, d, d, d)], q, B * T, d, d, bias=bq, post_scale=scale))
+            probs.append(_prob([_seg(kf, Wk, d, d, d)], k, B * Tk, d, d, bias=bk))
+            probs.append(_prob([_seg(kf, Wv, d, d, d, alpha_v)], v, B * Tk, d, d, bias=bv))
+            outs += [q, k, v]
+        gemm(L.GEMM_NT, probs)
+        ctx.G, ctx.cross, ctx.scale, ctx.alpha_v = G, cross, scale, alpha_v
+        ctx.save_for_backward(*xq, *(xkv if cross else []), *W)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        G, cross, scale, av = ctx.G, ctx.cross, ctx.scale, ctx.alpha_v
+        saved = ctx.saved_tensors
+        xq = saved[:G]
+        xkv = saved[G:2 * G] if cross else xq
+        W = saved[2 * G:] if cross else saved[G:]
+        B, T, d = xq[0].shape
+        Tk = xkv[0].shape[1]
+        refs = []
+        for g in range(G):
+            refs += [xq[g], xkv[g], xkv[g]]
+        grads = _contig(_zeros_for_none(grads, refs))
+        dxq, dxkv, probs = [], [], []
+        for g in range(G):
+            Wq, _, Wk, _, Wv, _ = W[6 * g:6 * g + 6]
+            dq, dk, dv = (_flat(t) for t in grads[3 * g:3 * g + 3])
+            gx = torch.empty_like(xq[g])
+            if cross:
+                gkv = torch.empty_like(xkv[g])
+                probs.append(_prob([_seg(dq, Wq, d, d, d, scale)], gx, B * T, d, d))
+                probs.append(_prob([_seg(dk, Wk, d, d, d), _seg(dv, Wv, d, d, d, av)], gkv, B * Tk, d, d))
+                dxkv.append(gkv)
+            else:
+                probs.append(_prob([_seg(dq, Wq, d, d, d, scale), _seg(dk, Wk, d, d, d), _seg(dv, Wv, d, d, d)],
+                                   gx, B * T, d, d))
+            dxq.append(gx)
+        gemm(L.GEMM_NN, probs)
+        items = []
+        for g in range(G):
+            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
+            dq, dk, dv = (_flat(t) for t in grads[3 * g:3 * g + 3])
+            xf, kf = _flat(xq[g]), _flat(xkv[g])
+            items += [(dq, xf, scale, Wq, bq is not None), (dk, kf, 1.0, Wk, bk is not None),
+                      (dv, kf, av, Wv, bv is not None, 1.0)]
+        wg = weight_grads(items)
+        dW = []
+        for g in range(G):
+            for j in range(3):
+                dW += list(wg[3 * g + j])
+        # note: dWv = (av*dV)^T kv  (alpha applied to A) == dV^T (kv/2) exactly
+        res = [None, None, None] + dxq + (dxkv if cross else []) + dW
+        return tuple(res)
+
+
+# --------------------------------------------------------------------------- attention core
+class KeyPaddingMask:
+    """The SCA mask contract without the B*T^2 materialisation: per-clip key validity
+    (B, Tk) as fp32 1/0 plus the causal flags.  Semantically identical to the additive masks
+    of model/utils.py:3-28 (see include/scatten.h for the exact score transform)."""
+
+    def __init__(self, mask, causal_plus_one=False):
+        if mask.dim() != 2:
+            raise ValueError("key padding mask must be (B, T)")
+        self.mask = mask
+        self.causal_plus_one = causal_plus_one
+        self.key_valid = (mask != 0).to(torch.float32).contiguous()
+
+    @property
+    def shape(self):
+        return self.mask.shape
+
+
+class AttentionCore(Function):
+    """O = softmax(q k^T + mask) v per head, heads interleaved in the channel dim."""
+
+    @staticmethod
+    def forward(ctx, G, H, causal, plus_one, key_valid, add_mask, *qkv):
+        q, k, v = _contig(qkv[:G]), _contig(qkv[G:2 * G]), _contig(qkv[2 * G:3 * G])
+        L.require_device(*q, *k, *v)
+        B, Tq, d = q[0].shape
+        Tk = k[0].shape[1]
+        hd = d // H
+        o = [torch.empty_like(t) for t in q]
+        sm = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+        sl = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+        for c in range(0, G, L.ATTN_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
+            arr = (L.AttnFwdProblem * len(gs))(*[
+                L.AttnFwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
+                                 sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask)) for g in gs])
+            fl = len(gs) * 4.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
+            with _timed("attn_fwd_kernel<%d>" % hd, fl):
+                L.check(L.lib().sca_attn_fwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal),
+                                             int(plus_one), L.stream_handle()), "sca_attn_fwd")
+        ctx.G, ctx.H, ctx.causal, ctx.plus_one = G, H, causal, plus_one
+        ctx.save_for_backward(key_valid, add_mask, *q, *k, *v, *o, *sm, *sl)
+        return tuple(o)
+
+    @staticmethod
+    def backward(ctx, *dout):
+        G, H = ctx.G, ctx.H
+        sv = ctx.saved_tensors
+        key_valid, add_mask = sv[0], sv[1]
+        q, k, v, o, sm, sl = (sv[2 + i * G:2 + (i + 1) * G] for i in range(6))
+        dout = _contig(_zeros_for_none(dout, o))
+        B, Tq, d = q[0].shape
+        Tk = k[0].shape[1]
+        hd = d // H
+        dq = [torch.empty_like(t) for t in q]
+        dk = [torch.empty_like(t) for t in k]
+        dv = [torch.empty_like(t) for t in v]
+        delta = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+        for c in range(0, G, L.ATTN_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
+            arr = (L.AttnBwdProblem * len(gs))(*[
+                L.AttnBwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
+                                 dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
+                                 ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
+                                 delta[g].data_ptr(), 1.0, 1.0) for g in gs])
+            fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if ctx.causal else Tq * Tk)
+            with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
+                L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(ctx.causal),
+                                             int(ctx.plus_one), L.stream_handle()), "sca_attn_bwd")
+        return (None,) * 6 + tuple(dq) + tuple(dk) + tuple(dv)
+
+
+# --------------------------------------------------------------------------- Linear (+ residual)
+class LinearResidual(Function):
+    """y = x W^T + b (+ r).  Out-projection of every attention op (attention.py:74) fused with
+    the post-LN residual add of keypoint_module.py:69-70 / :105-106 when r is given."""
+
+    @staticmethod
+    def forward(ctx, G, has_r, *ts):
+        x = _contig(ts[:G])
+        W, b = ts[G:2 * G], ts[2 * G:3 * G]
+        r = _contig(ts[3 * G:4 * G]) if has_r else [None] * G
+        L.require_device(*x)
+        probs, ys = [], []
+        for g in range(G):
+            n_out, n_in = W[g].shape
+            lead = x[g].shape[:-1]
+            M = x[g].numel() // n_in
+            y = x[g].new_empty(*lead, n_out)
+            probs.append(_prob([_seg(_flat(x[g]), W[g], n_in, n_in, n_in)], y, M, n_out, n_out, bias=b[g],
+                               resid=r[g], ldr=n_out))
+            ys.append(y)
+        gemm(L.GEMM_NT, probs)
+        ctx.G, ctx.has_r, ctx.has_b = G, has_r, [bb is not None for bb in b]
+        ctx.save_for_backward(*x, *W)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        G = ctx.G
+        sv = ctx.saved_tensors
+        x, W = sv[:G], sv[G:2 * G]
+        dys = _contig(_zeros_for_none(dys, [x[g].new_empty(*x[g].shape[:-1], W[g].shape[0]) for g in range(G)]))
+        probs, dxs = [], []
+        for g in range(G):
+            n_out, n_in = W[g].shape
+            M = x[g].numel() // n_in
+            dx = torch.empty_like(x[g])
+            probs.append(_prob([_seg(_flat(dys[g]), W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
+            dxs.append(dx)
+        gemm(L.GEMM_NN, probs)
+        wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.has_b[g]) for g in range(G)])
+        return (None, None) + tuple(dxs) + tuple(w for w, _ in wg) + tuple(bb for _, bb in wg) + \
+            (tuple(dys) if ctx.has_r else ())
+
+
+# --------------------------------------------------------------------------- FFN (+ residual)
+class FeedForwardResidual(Function):
+    """y = fc2(GELU(fc1 x)) (+ x when has_r)  (layers.py:94-108 with the residual of keypoint_module.py:71-72,
+    :108-109).  fc1's epilogue applies bias + exact-erf GELU and keeps the pre-activation; the
+    backward's dX GEMM of fc2 applies GELU' in its epilogue."""
+
+    @staticmethod
+    def forward(ctx, G, has_r, *ts):
+        x = _contig(ts[:G])
+        W1, b1, W2, b2 = ts[G:2 * G], ts[2 * G:3 * G], ts[3 * G:4 * G], ts[4 * G:5 * G]
+        L.require_device(*x)
+        B, T, d = x[0].shape
+        M = B * T
+        F_ = W1[0].shape[0]
+        zs = [x[0].new_empty(M, F_) for _ in range(G)]
+        acts = [x[0].new_empty(M, F_) for _ in range(G)]
+        gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
+                               epi=L.EPI_GELU, aux_out=zs[g], ldo=F_) for g in range(G)])
+        ys = [torch.empty_like(x[g]) for g in range(G)]
+        gemm(L.GEMM_NT, [_prob([_seg(acts[g], W2[g], F_, F_, F_)], ys[g], M, d, d, bias=b2[g],
+                               resid=_flat(x[g]) if has_r else None, ldr=d) for g in range(G)])
+        ctx.G, ctx.has_r = G, has_r
+        ctx.save_for_backward(*x, *W1, *W2, *zs, *acts)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        G = ctx.G
+        sv = ctx.saved_tensors
+        x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
+        dys = _contig(_zeros_for_none(dys, x))
+        B, T, d = x[0].shape
+        M = B * T
+        F_ = W1[0].shape[0]
+        dz = [x[0].new_empty(M, F_) for _ in range(G)]
+        # dz = (dy W2) * gelu'(z)
+        gemm(L.GEMM_NN, [_prob([_seg(_flat(dys[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
+                               aux=zs[g], ldx=F_) for g in range(G)])
+        # dx = dz W1 + dy   (residual)
+        dx = [torch.empty_like(x[g]) for g in range(G)]
+        gemm(L.GEMM_NN, [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
+                               resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)])
+        items = [(_flat(dys[g]), acts[g], 1.0, W2[g], True) for g in range(G)] + \
+                [(dz[g], _flat(x[g]), 1.0, W1[g], True) for g in range(G)]
+        wg = weight_grads(items)
+        dW2 = [wg[g] for g in range(G)]
+        dW1 = [wg[G + g] for g in range(G)]
+        return (None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
+            tuple(w for w, _ in dW2) + tuple(b for _, b in dW2)
+
+
+# --------------------------------------------------------------------------- LayerNorm
+class LayerNormAdd(Function):
+    """y = act(LayerNorm(x + r) + post).
+
+    r: None (plain LayerNorm) or the LearningPositionEmbedding table (layers.py:15-30), row
+       (t % T) + 2 of which is added to frame t;
+    post, act: the ResidualBlock tail relu(norm2(.) + residual) (model/residual.py:35-38),
+       or ReLU alone (norm1 -> relu, :32-33)."""
+
+    @staticmethod
+    def forward(ctx, G, eps, pos_table, has_post, act, *ts):
+        x = _contig(ts[:G])
+        o = G
+        tab = ts[o:o + G] if pos_table else [None] * G
+        o += G if pos_table else 0
+        post = _contig(ts[o:o + G]) if has_post else [None] * G
+        o += G if has_post else 0
+        gam, bet = ts[o:o + G], ts[o + G:o + 2 * G]
+        L.require_device(*x)
+        N = x[0].shape[-1]
+        rows = x[0].numel() // N
+        if pos_table:
+            T = x[0].shape[1]
+            if T + 2 > tab[0].shape[0]:
+                raise IndexError("index out of range in self")  # nn.Embedding past its table
+            r_mod, r_off = T, 2
+        else:
+            r_mod, r_off = max(rows, 1), 0
+        ys = [torch.empty_like(t) for t in x]
+        means = [x[0].new_empty(rows) for _ in range(G)]
+        rstds = [x[0].new_empty(rows) for _ in range(G)]
+        for c in range(0, G, L.LN_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
+            arr = (L.LnFwdProblem * len(gs))(*[L.LnFwdProblem(x[g].data_ptr(), ptr(tab[g]), gam[g].data_ptr(),
+                                                                bet[g].data_ptr(), ptr(post[g]), ys[g].data_ptr(),
+                                                                means[g].data_ptr(), rstds[g].data_ptr(), act)
+                                                 for g in gs])
+            L.check(L.lib().sca_layernorm_fwd(len(gs), arr, rows, N, r_mod, r_off, eps, L.stream_handle()),
+                    "sca_layernorm_fwd")
+        ctx.G, ctx.pos, ctx.has_post, ctx.act, ctx.r_mod, ctx.r_off = G, pos_table, has_post, act, r_mod, r_off
+        ctx.save_for_backward(*x, *(tab if pos_table else []), *gam, *means, *rstds, *(ys if act else []))
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        G, pos, act = ctx.G, ctx.pos, ctx.act
+        sv = list(ctx.saved_tensors)
+        x = sv[:G]
+        o = G
+        tab = sv[o:o + G] if pos else [None] * G
+        o += G if pos else 0
+        gam, means, rstds = sv[o:o + G], sv[o + G:o + 2 * G], sv[o + 2 * G:o + 3 * G]
+        ys = sv[o + 3 * G:o + 4 * G] if act else [None] * G
+        dys = _contig(_zeros_for_none(dys, x))
+        N = x[0].shape[-1]
+        rows = x[0].numel() // N
+        nblk = L.lib().sca_layernorm_bwd_blocks(rows)
+        dx = [torch.empty_like(t) for t in x]
+        dpost = [torch.empty_like(t) for t in x] if ctx.has_post else [None] * G
+        dg = [torch.empty_like(t) for t in gam]
+        db = [torch.empty_like(t) for t in gam]
+        part = [x[0].new_empty(2 * nblk * N) for _ in range(G)]
+        for c in range(0, G, L.LN_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
+            arr = (L.LnBwdProblem * len(gs))(*[L.LnBwdProblem(dys[g].data_ptr(), x[g].data_ptr(), ptr(tab[g]),
+                                                                gam[g].data_ptr(), means[g].data_ptr(),
+                                                                rstds[g].data_ptr(), ptr(ys[g]), act,
+                                                                ptr(dpost[g]), dx[g].data_ptr(), dg[g].data_ptr(),
+                                                                db[g].data_ptr(), part[g].data_ptr()) for g in gs])
+            L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, ctx.r_mod, ctx.r_off, 0, L.stream_handle()),
+                    "sca_layernorm_bwd")
+        dtab = []
+        if pos:
+            B, T = x[0].shape[0], x[0].shape[1]
+            dtab = [torch.zeros_like(t) for t in tab]
+            # d table[t + 2] = sum_b dv[b, t]
+            reduce_rows([(dx[g], dtab[g][2:], 1.0) for g in range(G)], B, T, N, T * N, N)
+        return (None,) * 5 + tuple(dx) + tuple(dtab) + (tuple(dpost) if ctx.has_post else ()) + \
+            tuple(dg) + tuple(db)
+
+
+class MaxPoolT(Function):
+    """MaxPool1d(2, 2) over the frame axis of (B, T, C) (model/residual.py:40-43)."""
+
+    @staticmethod
+    def forward(ctx, G, *xs):
+        xs = _contig(xs)
+        L.require_device(*xs)
+        B, T, C = xs[0].shape
+        ys = [x.new_empty(B, T // 2, C) for x in xs]
+        for c in range(0, G, L.POOL_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.POOL_MAX_PROBLEMS))
+            arr = (L.PoolProblem * len(gs))(*[L.PoolProblem(xs[g].data_ptr(), ys[g].data_ptr(), None, None)
+                                               for g in gs])
+            L.check(L.lib().sca_maxpool_t_fwd(len(gs), arr, B, T, C, L.stream_handle()), "sca_maxpool_t_fwd")
+        ctx.G = G
+        ctx.save_for_backward(*xs)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        G = ctx.G
+        xs = ctx.saved_tensors
+        B, T, C = xs[0].shape
+        dys = _contig(_zeros_for_none(dys, [x.new_empty(B, T // 2, C) for x in xs]))
+        dx = [torch.empty_like(x) for x in xs]
+        for c in range(0, G, L.POOL_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.POOL_MAX_PROBLEMS))
+            arr = (L.PoolProblem * len(gs))(*[L.PoolProblem(xs[g].data_ptr(), None, dys[g].data_ptr(),
+                                                             dx[g].data_ptr()) for g in gs])
+            L.check(L.lib().sca_maxpool_t_bwd(len(gs), arr, B, T, C, L.stream_handle()), "sca_maxpool_t_bwd")
+        return (None,) + tuple(dx)
+
+
+# --------------------------------------------------------------------------- coordinate mapping
+class CoordinateMappingOp(Function):
+    """Fused A1 + A2: slice each stream's joints out of the (B, T, K_all, 2) keypoints,
+    de-interleave x / y and apply the two Linear(K -> d) maps (layers.py:111-123)."""
+
+    @staticmethod
+    def forward(ctx, G, kp, *ts):
+        idx = ts[:G]
+        Wx, bx, Wy, by = ts[G:2 * G], ts[2 * G:3 * G], ts[3 * G:4 * G], ts[4 * G:5 * G]
+        kpc = kp.contiguous()
+        L.require_device(kpc)
+        B, T, K_all, _ = kpc.shape
+        rows = B * T
+        N = Wx[0].shape[0]
+        xe = [kpc.new_empty(B, T, N) for _ in range(G)]
+        ye = [kpc.new_empty(B, T, N) for _ in range(G)]
+        for c in range(0, G, L.MAP_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.MAP_MAX_PROBLEMS))
+            arr = (L.CoordMapProblem * len(gs))(*[
+                L.CoordMapProblem(kpc.data_ptr(), idx[g].data_ptr(), idx[g].numel(), Wx[g].data_ptr(), ptr(bx[g]),
+                                  Wy[g].data_ptr(), ptr(by[g]), xe[g].data_ptr(), ye[g].data_ptr()) for g in gs])
+            L.check(L.lib().sca_coord_map_fwd(len(gs), arr, rows, K_all, N, L.stream_handle()), "sca_coord_map_fwd")
+        ctx.G = G
+        ctx.kp_grad = kp.requires_grad
+        ctx.has_b = [b is not None for b in bx]
+        ctx.save_for_backward(kpc, *idx, *Wx, *Wy)
+        return tuple(xe) + tuple(ye)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        G = ctx.G
+        sv = ctx.saved_tensors
+        kp = sv[0]
+        idx, Wx, Wy = sv[1:1 + G], sv[1 + G:1 + 2 * G], sv[1 + 2 * G:1 + 3 * G]
+        B, T, K_all, _ = kp.shape
+        rows = B * T
+        N = Wx[0].shape[0]
+        refs = [kp.new_empty(B, T, N)] * (2 * G)
+        grads = _contig(_zeros_for_none(grads, refs))
+        dxe, dye = grads[:G], grads[G:]
+        dwx = [torch.empty_like(w) for w in Wx]
+        dwy = [torch.empty_like(w) for w in Wy]
+        dkp = torch.zeros_like(kp) if ctx.kp_grad else None
+        nchunk = L.lib().sca_coord_map_bwd_chunks(rows)
+        part = [kp.new_empty(2 * nchunk * N * idx[g].numel()) for g in range(G)]
+        for c in range(0, G, L.MAP_MAX_PROBLEMS):
+            gs = range(c, min(G, c + L.MAP_MAX_PROBLEMS))
+            arr = (L.CoordMapBwdProblem * len(gs))(*[
+                L.CoordMapBwdProblem(kp.data_ptr(), idx[g].data_ptr(), idx[g].numel(), Wx[g].data_ptr(),
+                                     Wy[g].data_ptr(), dxe[g].data_ptr(), dye[g].data_ptr(), dwx[g].data_ptr(),
+                                     dwy[g].data_ptr(), ptr(dkp), part[g].data_ptr()) for g in gs])
+            L.check(L.lib().sca_coord_map_bwd(len(gs), arr, rows, K_all, N, L.stream_handle()), "sca_coord_map_bwd")
+        dbx = [kp.new_empty(N) if ctx.has_b[g] else None for g in range(G)]
+        dby = [kp.new_empty(N) if ctx.has_b[g] else None for g in range(G)]
+        pairs = [(dxe[g], dbx[g], 1.0) for g in range(G) if dbx[g] is not None] + \
+                [(dye[g], dby[g], 1.0) for g in range(G) if dby[g] is not None]
+        if pairs:
+            reduce_rows(pairs, rows, 1, N, N, 0)
+        return (None, dkp) + (None,) * G + tuple(dwx) + tuple(dbx) + tuple(dwy) + tuple(dby)

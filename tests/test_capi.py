@@ -1,0 +1,70 @@
+"""The C-ABI library loads and exports every entry point declared in include/*.h, and the
+product path refuses to run anywhere but on the GPU (no silent CPU fallback).  CPU only."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(sca_\w+)\s*\(", src, flags=re.M))
+    return sorted(names)
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "sca_gemm" in names and "sca_attn_fwd" in names and "sca_attn_bwd" in names
+    assert len(names) >= 12
+
+
+def test_library_exports_every_declared_symbol():
+    from scattennet_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+    # every declared symbol is bound with a signature by the Python layer
+    assert set(_declared()) - {"sca_set_error"} <= set(_lib.EXPORTS), set(_declared()) - set(_lib.EXPORTS)
+
+
+def test_struct_sizes_match_header_layout():
+    """ctypes mirrors of the C structs: pointer-aligned sizes the kernels rely on."""
+    from scattennet_amd import _lib as L
+    assert ctypes.sizeof(L.GemmSeg) == 32
+    assert ctypes.sizeof(L.GemmProblem) % 8 == 0
+    assert ctypes.sizeof(L.AttnFwdProblem) == 64
+
+
+def test_cpu_tensors_are_rejected():
+    import scattennet_amd as S
+    m = S.SelfAttention(32, 2)
+    x = torch.randn(1, 8, 32)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(x, S.key_padding_mask(torch.ones(1, 8, dtype=torch.long)))
+
+
+def test_constructor_errors_match_reference():
+    import scattennet_amd as S
+    with pytest.raises(ValueError):
+        S.SelfAttention(30, 4)
+    with pytest.raises(ValueError):
+        S.CoordinateAttention({"d_model": 32, "attention_heads": 2, "attention_dropout": 0.0, "dropout": 0.0,
+                               "ff_dim": 64}, "bogus")
+
+
+def test_state_dict_keys_match_reference():
+    """Key layout of one KeypointModule equals the reference's (golden fixture keys)."""
+    import scattennet_amd as S
+    from tests.golden_util import load
+    fx = load("keypoint_module")
+    m = S.KeypointModule(list(range(3, 24)), fx["meta"]["T"], fx["meta"]["cfg"])
+    assert set(m.state_dict().keys()) == set(fx["param"].keys())
+    m.load_state_dict(fx["param"])  # strict
