@@ -74,12 +74,16 @@ typedef struct {
   int ldx;
   float* aux_out; /* GELU pre-activation output [M, ldo] */
   int ldo;
+  /* TN layout only: bias_grad[m] = bias_grad_scale * sum_k alpha*A[k, m] (the Linear bias
+   * gradient colsum(dY), fused into the weight-gradient GEMM), or NULL */
+  float* bias_grad;
+  float bias_grad_scale;
 } sca_gemm_problem;
 
 /* Grouped GEMM over `nprob` independent problems (e.g. q/k/v x streams).
  * splitk > 1 (TN layout, single segment only) writes fp32 partial slabs into
- * `workspace` (nprob * splitk * M * N floats, problems must share M and N) and reduces
- * them in a second launch in fixed order (deterministic).                               */
+ * `workspace` (nprob * splitk * (M * N + M) floats, problems must share M and N) and
+ * reduces them in a second launch in fixed order (deterministic).                       */
 int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
              void* stream);
 

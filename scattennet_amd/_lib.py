@@ -32,7 +32,8 @@ class GemmSeg(ctypes.Structure):
 class GemmProblem(ctypes.Structure):
     _fields_ = [("seg", GemmSeg * 3), ("nseg", c_int), ("M", c_int), ("N", c_int), ("C", c_void_p), ("ldc", c_int),
                 ("epi", c_int), ("bias", c_void_p), ("post_scale", c_float), ("resid", c_void_p), ("ldr", c_int),
-                ("aux", c_void_p), ("ldx", c_int), ("aux_out", c_void_p), ("ldo", c_int)]
+                ("aux", c_void_p), ("ldx", c_int), ("aux_out", c_void_p), ("ldo", c_int), ("bias_grad", c_void_p),
+                ("bias_grad_scale", c_float)]
 
 
 class AttnFwdProblem(ctypes.Structure):

@@ -66,32 +66,26 @@ def _resolve_mask(mask, causal):
     raise TypeError(f"unsupported attention_mask type {type(mask)}")
 
 
-def attention_grouped(attns, kind, hidden, kv, mask, resid=None):
+def attention_grouped(attns, kind, hidden, kv, mask, resid=False):
     """Run G attention operators of the same shape in lock-step (one launch per stage).
 
-    kind: "self" | "causal" | "cross".  Returns out_proj(attn) (+ resid when given, the
-    post-LN residual of the enclosing block fused into the out-projection epilogue)."""
+    kind: "self" | "causal" | "cross".  Returns out_proj(attn), plus the operator's own
+    query input when `resid` (the post-LN residual of the enclosing block, fused into the
+    out-projection epilogue)."""
     G = len(attns)
     a0 = attns[0]
     for a in attns:
         if a.training and a.dropout > 0:
             raise NotImplementedError("attention dropout > 0 in training mode is not implemented")
+    causal = kind == "causal"
+    key_valid, add_mask, plus_one = _resolve_mask(mask, causal)
     params = []
     for a in attns:
         params += a.qkv_params()
-    if kind == "cross":
-        qkv = ops.QKVProjection.apply(G, True, a0.scaling, *hidden, *kv, *params)
-    else:
-        qkv = ops.QKVProjection.apply(G, False, a0.scaling, *hidden, *params)
-    q, k, v = qkv[0::3], qkv[1::3], qkv[2::3]
-    causal = kind == "causal"
-    key_valid, add_mask, plus_one = _resolve_mask(mask, causal)
-    o = ops.AttentionCore.apply(G, a0.num_heads, causal, plus_one, key_valid, add_mask, *q, *k, *v)
-    Wo = [a.out_proj.weight for a in attns]
-    bo = [a.out_proj.bias for a in attns]
-    if resid is None:
-        return list(ops.LinearResidual.apply(G, False, *o, *Wo, *bo))
-    return list(ops.LinearResidual.apply(G, True, *o, *Wo, *bo, *resid))
+    ts = list(hidden) + (list(kv) if kind == "cross" else []) + params + \
+        [a.out_proj.weight for a in attns] + [a.out_proj.bias for a in attns]
+    return list(ops.AttentionBlock.apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
+                                         bool(resid), *ts))
 
 
 class SelfAttention(BaseAttention):

@@ -151,6 +151,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   f32x4 ra[OpA::kVec], rb[OpB::kVec];
+  // fused bias gradient (TN): the first column tile sums its A slices (= alpha * dY rows)
+  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && blockIdx.x == 0;
+  float bsum = 0.f;
 
   for (int sidx = 0; sidx < P.nseg; ++sidx) {
     const sca_gemm_seg S = P.seg[sidx];
@@ -172,6 +175,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
         load_tile<A_KC, BM>(ra, S.A, S.lda, m0, P.M, k0 + BK, kend, S.alpha);
         load_tile<B_KC, BN>(rb, S.B, S.ldb, n0, P.N, k0 + BK, kend, 1.0f);
       }
+      if (do_bias && threadIdx.x < BM) {
+#pragma unroll 8
+        for (int k = 0; k < BK; ++k) bsum += As[k * (BM + 4) + threadIdx.x];  // TN: A image is [BK][BM+4]
+      }
 #pragma unroll
       for (int g8 = 0; g8 < BK / 8; ++g8) {
         f32x4 fa[RM], fb[RN];
@@ -192,6 +199,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
   // C/D map of v_mfma_f32_32x32x2_f32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
   const int col = lane & 31;
   const int rowh = 4 * (lane >> 5);
+  if (do_bias && threadIdx.x < BM && m0 + (int)threadIdx.x < P.M) {
+    if (splitk > 1)
+      args.ws[(long)gridDim.z * P.M * P.N + (long)blockIdx.z * P.M + m0 + threadIdx.x] = bsum;
+    else
+      P.bias_grad[m0 + threadIdx.x] = bsum * P.bias_grad_scale;
+  }
   if (splitk > 1) {
     float* slab = args.ws + (long)blockIdx.z * P.M * P.N;
 #pragma unroll
@@ -218,12 +231,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
       }
 }
 
-// Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]).
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args) {
+// Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]); bias partials likewise.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args, int nprob) {
   const sca_gemm_problem& P = args.p[blockIdx.y];
   const long MN = (long)P.M * P.N;
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= MN) return;
+  if (e >= MN) {
+    const long m = e - MN;
+    if (P.bias_grad && m < P.M) {
+      const float* bp = args.ws + (long)nprob * args.splitk * MN + (long)blockIdx.y * args.splitk * P.M + m;
+      float v = 0.f;
+      for (int s = 0; s < args.splitk; ++s) v += bp[(long)s * P.M];
+      P.bias_grad[m] = v * P.bias_grad_scale;
+    }
+    return;
+  }
   const int m = (int)(e / P.N), n = (int)(e % P.N);
   const float* slab = args.ws + (long)blockIdx.y * args.splitk * MN + e;
   float v = 0.f;
@@ -274,6 +296,7 @@ extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, in
     }
     if ((P.epi & SCA_EPI_GELU) && !P.aux_out) { sca_set_error("sca_gemm: GELU needs aux_out"); return SCA_ERR_ARG; }
     if ((P.epi & SCA_EPI_DGELU) && !P.aux) { sca_set_error("sca_gemm: DGELU needs aux"); return SCA_ERR_ARG; }
+    if (P.bias_grad && layout != SCA_GEMM_TN) { sca_set_error("sca_gemm: bias_grad only with TN"); return SCA_ERR_ARG; }
     if (splitk > 1 && (P.nseg != 1 || P.M != probs[0].M || P.N != probs[0].N)) {
       sca_set_error("sca_gemm: split-K needs one segment and equal M,N");
       return SCA_ERR_ARG;
@@ -294,8 +317,8 @@ extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, in
   if (rc != SCA_OK) { sca_set_error("sca_gemm: launch failed"); return rc; }
   if (splitk > 1) {
     const long MN = (long)maxM * maxN;
-    dim3 grid((unsigned)((MN + 255) / 256), nprob);
-    hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, a);
+    dim3 grid((unsigned)((MN + maxM + 255) / 256), nprob);
+    hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, a, nprob);
     if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm: reduce launch failed"); return SCA_ERR_LAUNCH; }
   }
   return SCA_OK;

@@ -25,115 +25,157 @@ constexpr int LN_MAXV = 16;  // values per lane -> N <= 1024
 
 __device__ __forceinline__ long rrow(int row, int r_mod, int r_off) { return (long)(row % r_mod) + r_off; }
 
+// Row element access: NV > 0 -> N = 256*NV, lane owns float4 columns 4*lane + 256*j (16 B/lane
+// loads); NV == 0 -> any N <= 1024, lane owns scalar columns lane + 64*j.
+template <int NV>
+struct RowMap {
+  static constexpr int kVals = NV > 0 ? 4 * NV : LN_MAXV;
+  __device__ static __forceinline__ int col(int lane, int i) {
+    return NV > 0 ? 4 * lane + 256 * (i >> 2) + (i & 3) : lane + 64 * i;
+  }
+};
+
+template <int NV>
+__device__ __forceinline__ void load_row(float* v, const float* p, int lane, int N) {
+  if (NV > 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const f32x4 t = ld4(p + 4 * lane + 256 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * j + e] = t[e];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < N ? p[c] : 0.f;
+    }
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void store_row(float* p, const float* v, int lane, int N) {
+  if (NV > 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) st4(p + 4 * lane + 256 * j, f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]});
+  } else {
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < N) p[c] = v[i];
+    }
+  }
+}
+
+template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const LnFwdArgs a) {
+  using RM = RowMap<NV>;
+  constexpr int V = RM::kVals;
   const sca_ln_fwd_problem& P = a.p[blockIdx.y];
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.rows) return;
   const int N = a.N;
-  const float* xr = P.x + (long)row * N;
-  const float* rr = P.r ? P.r + rrow(row, a.r_mod, a.r_off) * N : nullptr;
-  float v[LN_MAXV];
+  float v[V], t[V];
+  load_row<NV>(v, P.x + (long)row * N, lane, N);
+  if (P.r) {
+    load_row<NV>(t, P.r + rrow(row, a.r_mod, a.r_off) * N, lane, N);
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] += t[i];
+  }
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = lane + 64 * j;
-    float t = 0.f;
-    if (c < N) {
-      t = xr[c];
-      if (rr) t += rr[c];
-    }
-    v[j] = t;
-    s += t;
-  }
+  for (int i = 0; i < V; ++i) s += v[i];
   const float mean = wave_sum(s) / N;
   float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = lane + 64 * j;
-    if (c < N) {
-      const float d = v[j] - mean;
-      q += d * d;
-    }
+  for (int i = 0; i < V; ++i) {
+    const float d = (NV > 0 || RM::col(lane, i) < N) ? v[i] - mean : 0.f;
+    q += d * d;
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / N + a.eps);
-  float* yr = P.y + (long)row * N;
-  const float* pr = P.post ? P.post + (long)row * N : nullptr;
+  float g[V], b[V];
+  load_row<NV>(g, P.gamma, lane, N);
+  load_row<NV>(b, P.beta, lane, N);
+  if (P.post) load_row<NV>(t, P.post + (long)row * N, lane, N);
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = lane + 64 * j;
-    if (c < N) {
-      float o = (v[j] - mean) * rstd * P.gamma[c] + P.beta[c];
-      if (pr) o += pr[c];
-      if (P.act == SCA_ACT_RELU) o = fmaxf(o, 0.f);
-      yr[c] = o;
-    }
+  for (int i = 0; i < V; ++i) {
+    float o = (v[i] - mean) * rstd * g[i] + b[i];
+    if (P.post) o += t[i];
+    if (P.act == SCA_ACT_RELU) o = fmaxf(o, 0.f);
+    v[i] = o;
   }
+  store_row<NV>(P.y + (long)row * N, v, lane, N);
   if (lane == 0) {
     P.mean[row] = mean;
     P.rstd[row] = rstd;
   }
 }
 
-constexpr int LN_BWD_ROWS = 32;  // rows per workgroup (8 per wave)
+constexpr int LN_BWD_ROWS = 16;  // rows per workgroup (4 per wave)
 
+template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const LnBwdArgs a) {
+  using RM = RowMap<NV>;
+  constexpr int V = RM::kVals;
   const sca_ln_bwd_problem& P = a.p[blockIdx.y];
   __shared__ float red[2][4][1024];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int N = a.N;
-  float pg[LN_MAXV], pb[LN_MAXV];
+  float pg[V], pb[V], gam[V];
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) pg[j] = pb[j] = 0.f;
-  const int rbeg = blockIdx.x * LN_BWD_ROWS;
-  for (int i = w; i < LN_BWD_ROWS; i += 4) {
-    const int row = rbeg + i;
+  for (int i = 0; i < V; ++i) pg[i] = pb[i] = 0.f;
+  load_row<NV>(gam, P.gamma, lane, N);
+  const int rbeg = blockIdx.x * LN_BWD_ROWS + w * (LN_BWD_ROWS / 4);
+#pragma unroll
+  for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
+    const int row = rbeg + rr;
     if (row >= a.rows) break;
     const float mean = P.mean[row], rstd = P.rstd[row];
-    const float* xr = P.x + (long)row * N;
-    const float* rr = P.r ? P.r + rrow(row, a.r_mod, a.r_off) * N : nullptr;
-    const float* dyr = P.dy + (long)row * N;
-    const float* yr = P.act ? P.y + (long)row * N : nullptr;
-    float* dpr = P.dpost ? P.dpost + (long)row * N : nullptr;
-    float xh[LN_MAXV], g[LN_MAXV];
+    float xv[V], dy[V], t[V];
+    load_row<NV>(xv, P.x + (long)row * N, lane, N);
+    if (P.r) {
+      load_row<NV>(t, P.r + rrow(row, a.r_mod, a.r_off) * N, lane, N);
+#pragma unroll
+      for (int i = 0; i < V; ++i) xv[i] += t[i];
+    }
+    load_row<NV>(dy, P.dy + (long)row * N, lane, N);
+    if (P.act) {
+      load_row<NV>(t, P.y + (long)row * N, lane, N);
+#pragma unroll
+      for (int i = 0; i < V; ++i)
+        if (!(t[i] > 0.f)) dy[i] = 0.f;  // ReLU gate (threshold_backward: out > 0)
+    }
+    if (P.dpost) store_row<NV>(P.dpost + (long)row * N, dy, lane, N);
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int j = 0; j < LN_MAXV; ++j) {
-      const int c = lane + 64 * j;
-      xh[j] = g[j] = 0.f;
-      if (c < N) {
-        float t = xr[c];
-        if (rr) t += rr[c];
-        float dy = dyr[c];
-        if (yr && !(yr[c] > 0.f)) dy = 0.f;  // ReLU gate (threshold_backward: out > 0)
-        if (dpr) dpr[c] = dy;
-        xh[j] = (t - mean) * rstd;
-        g[j] = dy * P.gamma[c];
-        sg += g[j];
-        sgx += g[j] * xh[j];
-        pg[j] += dy * xh[j];
-        pb[j] += dy;
-      }
+    for (int i = 0; i < V; ++i) {
+      const bool in = NV > 0 || RM::col(lane, i) < N;
+      xv[i] = in ? (xv[i] - mean) * rstd : 0.f;  // x-hat
+      const float g = dy[i] * gam[i];
+      sg += g;
+      sgx += g * xv[i];
+      pg[i] += dy[i] * xv[i];
+      pb[i] += dy[i];
     }
     const float mg = wave_sum(sg) / N, mgx = wave_sum(sgx) / N;
     float* dxr = P.dx + (long)row * N;
+    if (a.accumulate) load_row<NV>(t, dxr, lane, N);
 #pragma unroll
-    for (int j = 0; j < LN_MAXV; ++j) {
-      const int c = lane + 64 * j;
-      if (c < N) {
-        float d = rstd * (g[j] - mg - xh[j] * mgx);
-        if (a.accumulate) d += dxr[c];
-        dxr[c] = d;
-      }
+    for (int i = 0; i < V; ++i) {
+      float d = rstd * (dy[i] * gam[i] - mg - xv[i] * mgx);
+      if (a.accumulate) d += t[i];
+      t[i] = d;
     }
+    store_row<NV>(dxr, t, lane, N);
   }
   // combine the 4 waves' partials in fixed order, one partial row per workgroup
 #pragma unroll
-  for (int j = 0; j < LN_MAXV; ++j) {
-    const int c = lane + 64 * j;
+  for (int i = 0; i < V; ++i) {
+    const int c = RM::col(lane, i);
     if (c < N) {
-      red[0][w][c] = pg[j];
-      red[1][w][c] = pb[j];
+      red[0][w][c] = pg[i];
+      red[1][w][c] = pb[i];
     }
   }
   __syncthreads();
@@ -371,7 +413,14 @@ extern "C" int sca_layernorm_fwd(int nprob, const sca_ln_fwd_problem* probs, int
   for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
   a.rows = rows; a.N = N; a.r_mod = r_mod; a.r_off = r_off; a.eps = eps;
   dim3 grid((rows + 3) / 4, nprob);
-  hipLaunchKernelGGL(ln_fwd_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (N % 256 == 0 ? N / 256 : 0) {
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(ln_fwd_kernel<0>, grid, dim3(256), 0, st, a); break;
+  }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_layernorm_fwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
@@ -421,7 +470,13 @@ extern "C" int sca_layernorm_bwd(int nprob, const sca_ln_bwd_problem* probs, int
   a.rows = rows; a.N = N; a.r_mod = r_mod; a.r_off = r_off; a.accumulate = accumulate;
   a.nblk = sca_layernorm_bwd_blocks(rows);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(a.nblk, nprob), dim3(256), 0, st, a);
+  switch (N % 256 == 0 ? N / 256 : 0) {
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<0>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
+  }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_layernorm_bwd: launch failed"); return SCA_ERR_LAUNCH; }
   // dgamma / dbeta = fixed-order sums of the per-workgroup partial rows
   ReduceArgs r;
@@ -486,7 +541,9 @@ extern "C" int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* pro
   a.rows = rows; a.K_all = K_all; a.N = N; a.nchunk = sca_coord_map_bwd_chunks(rows);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(coord_map_bwd_w_kernel, dim3(a.nchunk, nprob), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(coord_map_bwd_kp_kernel, dim3((rows + 3) / 4, nprob), dim3(256), 0, st, a);
+  bool any_dkp = false;
+  for (int i = 0; i < nprob; ++i) any_dkp |= probs[i].dkp != nullptr;
+  if (any_dkp) hipLaunchKernelGGL(coord_map_bwd_kp_kernel, dim3((rows + 3) / 4, nprob), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_coord_map_bwd: launch failed"); return SCA_ERR_LAUNCH; }
   // dW = fixed-order sum over row chunks (problems may differ in K: one reduce each)
   for (int i = 0; i < nprob; ++i) {

@@ -48,7 +48,7 @@ def coordinate_attention_grouped(blocks, xs, mask):
     The residual adds ride in the out-projection / fc2 epilogues."""
     check_dropout(blocks)
     kind = "self" if blocks[0].attn_type == "self_attn" else "causal"
-    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=xs)
+    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=True)
     h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
     if kind == "self":
         h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
@@ -75,7 +75,7 @@ class CoordinatesMerge(nn.Module):
 
 def coordinates_merge_grouped(blocks, ys, xs, mask):
     check_dropout(blocks)
-    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=ys)
+    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True)
     h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
     h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
     return layernorm_grouped([b.last_layer_norm for b in blocks], h)

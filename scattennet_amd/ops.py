@@ -76,10 +76,10 @@ def _seg(A, B, lda, ldb, K, alpha=1.0):
 
 
 def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=0, aux=None, ldx=0,
-          aux_out=None, ldo=0):
+          aux_out=None, ldo=0, bias_grad=None, bias_grad_scale=1.0):
     s = list(segs) + [_NOSEG] * (3 - len(segs))
     return L.GemmProblem((L.GemmSeg * 3)(*s), len(segs), M, N, C.data_ptr(), ldc, epi, ptr(bias), post_scale,
-                         ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo)
+                         ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo, ptr(bias_grad), bias_grad_scale)
 
 
 def gemm(layout, probs, splitk=1, ws=None):
@@ -114,7 +114,8 @@ def _splitk_for(M_red, n_out_tiles):
 
 
 def weight_grads(items, M=None):
-    """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = alpha_g * colsum(dY_g).
+    """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
+    the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
 
     items: list of (dY[M,out], X[M,in], alpha, W_like, has_bias[, bias_scale]) -> [(dW, db)].
     bias_scale defaults to alpha; it differs when alpha scales the INPUT X (v from kv/2:
@@ -135,18 +136,14 @@ def weight_grads(items, M=None):
             sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
             probs = []
             for i in sub:
-                dY, X, alpha, W, _, _ = items[i]
-                probs.append(_prob([_seg(dY, X, n_out, n_in, Mr, alpha)], out[i][0], n_out, n_in, n_in))
+                dY, X, alpha, W, _, bscale = items[i]
+                probs.append(_prob([_seg(dY, X, n_out, n_in, Mr, alpha)], out[i][0], n_out, n_in, n_in,
+                                   bias_grad=out[i][1], bias_grad_scale=bscale / alpha))
             ws = None
             if sk > 1:
-                ws = torch.empty(len(sub) * sk * n_out * n_in, device=items[0][0].device, dtype=torch.float32)
+                ws = torch.empty(len(sub) * sk * (n_out * n_in + n_out), device=items[0][0].device,
+                                 dtype=torch.float32)
             gemm(L.GEMM_TN, probs, splitk=sk, ws=ws)
-    by_w = {}  # bias grads, grouped by (width, rows)
-    for i, (dY, _, _, _, _, bscale) in enumerate(items):
-        if out[i][1] is not None:
-            by_w.setdefault((dY.shape[1], dY.shape[0]), []).append((dY, out[i][1], bscale))
-    for (w, Mr), ps in by_w.items():
-        reduce_rows(ps, Mr, 1, w, w, 0)
     return out
 
 
@@ -162,85 +159,7 @@ def _zeros_for_none(grads, refs):
     return [g if g is not None else torch.zeros_like(r) for g, r in zip(grads, refs)]
 
 
-# --------------------------------------------------------------------------- q/k/v projections
-class QKVProjection(Function):
-    """q = (x_q Wq^T + bq) * scale ; k = x_kv Wk^T + bk ; v = (alpha_v * x_kv) Wv^T + bv.
-
-    self/causal attention: x_kv is x_q (attention.py:49-51, :151-153);
-    cross attention: x_q = hidden_states, x_kv = key_value_states, alpha_v = 0.5 (:101-103)."""
-
-    @staticmethod
-    def forward(ctx, G, cross, scale, *ts):
-        xq = _contig(ts[:G])
-        xkv = _contig(ts[G:2 * G]) if cross else xq
-        W = ts[2 * G:] if cross else ts[G:]
-        L.require_device(*xq, *xkv)
-        B, T, d = xq[0].shape
-        Tk = xkv[0].shape[1]
-        alpha_v = 0.5 if cross else 1.0
-        outs = []
-        probs = []
-        for g in range(G):
-            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
-            xf, kf = _flat(xq[g]), _flat(xkv[g])
-            q = xq[g].new_empty(B, T, d)
-            k = xq[g].new_empty(B, Tk, d)
-            v = xq[g].new_empty(B, Tk, d)
-            probs.append(_prob([_seg(xf, Wq, d, d, d)], q, B * T, d, d, bias=bq, post_scale=scale))
-            probs.append(_prob([_seg(kf, Wk, d, d, d)], k, B * Tk, d, d, bias=bk))
-            probs.append(_prob([_seg(kf, Wv, d, d, d, alpha_v)], v, B * Tk, d, d, bias=bv))
-            outs += [q, k, v]
-        gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.cross, ctx.scale, ctx.alpha_v = G, cross, scale, alpha_v
-        ctx.save_for_backward(*xq, *(xkv if cross else []), *W)
-        return tuple(outs)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        G, cross, scale, av = ctx.G, ctx.cross, ctx.scale, ctx.alpha_v
-        saved = ctx.saved_tensors
-        xq = saved[:G]
-        xkv = saved[G:2 * G] if cross else xq
-        W = saved[2 * G:] if cross else saved[G:]
-        B, T, d = xq[0].shape
-        Tk = xkv[0].shape[1]
-        refs = []
-        for g in range(G):
-            refs += [xq[g], xkv[g], xkv[g]]
-        grads = _contig(_zeros_for_none(grads, refs))
-        dxq, dxkv, probs = [], [], []
-        for g in range(G):
-            Wq, _, Wk, _, Wv, _ = W[6 * g:6 * g + 6]
-            dq, dk, dv = (_flat(t) for t in grads[3 * g:3 * g + 3])
-            gx = torch.empty_like(xq[g])
-            if cross:
-                gkv = torch.empty_like(xkv[g])
-                probs.append(_prob([_seg(dq, Wq, d, d, d, scale)], gx, B * T, d, d))
-                probs.append(_prob([_seg(dk, Wk, d, d, d), _seg(dv, Wv, d, d, d, av)], gkv, B * Tk, d, d))
-                dxkv.append(gkv)
-            else:
-                probs.append(_prob([_seg(dq, Wq, d, d, d, scale), _seg(dk, Wk, d, d, d), _seg(dv, Wv, d, d, d)],
-                                   gx, B * T, d, d))
-            dxq.append(gx)
-        gemm(L.GEMM_NN, probs)
-        items = []
-        for g in range(G):
-            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
-            dq, dk, dv = (_flat(t) for t in grads[3 * g:3 * g + 3])
-            xf, kf = _flat(xq[g]), _flat(xkv[g])
-            items += [(dq, xf, scale, Wq, bq is not None), (dk, kf, 1.0, Wk, bk is not None),
-                      (dv, kf, av, Wv, bv is not None, 1.0)]
-        wg = weight_grads(items)
-        dW = []
-        for g in range(G):
-            for j in range(3):
-                dW += list(wg[3 * g + j])
-        # note: dWv = (av*dV)^T kv  (alpha applied to A) == dV^T (kv/2) exactly
-        res = [None, None, None] + dxq + (dxkv if cross else []) + dW
-        return tuple(res)
-
-
-# --------------------------------------------------------------------------- attention core
+# --------------------------------------------------------------------------- attention
 class KeyPaddingMask:
     """The SCA mask contract without the B*T^2 materialisation: per-clip key validity
     (B, Tk) as fp32 1/0 plus the causal flags.  Semantically identical to the additive masks
@@ -258,58 +177,150 @@ class KeyPaddingMask:
         return self.mask.shape
 
 
-class AttentionCore(Function):
-    """O = softmax(q k^T + mask) v per head, heads interleaved in the channel dim."""
+def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v):
+    B, Tq, d = q[0].shape
+    Tk = k[0].shape[1]
+    hd = d // H
+    o = [torch.empty_like(t) for t in q]
+    sm = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+    sl = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+    for c in range(0, G, L.ATTN_MAX_PROBLEMS):
+        gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
+        arr = (L.AttnFwdProblem * len(gs))(*[
+            L.AttnFwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
+                             sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask)) for g in gs])
+        fl = len(gs) * 4.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
+        with _timed("attn_fwd_kernel<%d>" % hd, fl):
+            L.check(L.lib().sca_attn_fwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
+                                         L.stream_handle()), "sca_attn_fwd")
+    return o, sm, sl
+
+
+def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, dout):
+    B, Tq, d = q[0].shape
+    Tk = k[0].shape[1]
+    hd = d // H
+    dq = [torch.empty_like(t) for t in q]
+    dk = [torch.empty_like(t) for t in k]
+    dv = [torch.empty_like(t) for t in v]
+    delta = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+    for c in range(0, G, L.ATTN_MAX_PROBLEMS):
+        gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
+        arr = (L.AttnBwdProblem * len(gs))(*[
+            L.AttnBwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
+                             dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
+                             ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
+                             delta[g].data_ptr(), 1.0, 1.0) for g in gs])
+        fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
+        with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
+            L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
+                                         L.stream_handle()), "sca_attn_bwd")
+    return dq, dk, dv
+
+
+class AttentionBlock(Function):
+    """One attention operator end to end, G streams per launch:
+
+        q = (x_q Wq^T + bq) * scale ; k = x_kv Wk^T + bk ; v = (alpha_v x_kv) Wv^T + bv
+        o = softmax(q k^T + mask) v      (per head; fused kernel, nothing T^2 in HBM)
+        y = o Wo^T + bo (+ x_q)          (the enclosing post-LN block's residual, fused)
+
+    kinds: "self" (attention.py:46-76), "causal" (:148-182), "cross" (:97-128, x_kv =
+    key_value_states, alpha_v = 0.5 reproduces v_proj(kv / 2)).  The backward fuses the
+    residual gradient into the dX GEMM epilogue and all of the block's weight/bias gradients
+    into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, H, causal, plus_one, key_valid, add_mask, *qkv):
-        q, k, v = _contig(qkv[:G]), _contig(qkv[G:2 * G]), _contig(qkv[2 * G:3 * G])
-        L.require_device(*q, *k, *v)
-        B, Tq, d = q[0].shape
-        Tk = k[0].shape[1]
-        hd = d // H
-        o = [torch.empty_like(t) for t in q]
-        sm = [q[0].new_empty(B * H * Tq) for _ in range(G)]
-        sl = [q[0].new_empty(B * H * Tq) for _ in range(G)]
-        for c in range(0, G, L.ATTN_MAX_PROBLEMS):
-            gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
-            arr = (L.AttnFwdProblem * len(gs))(*[
-                L.AttnFwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
-                                 sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask)) for g in gs])
-            fl = len(gs) * 4.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
-            with _timed("attn_fwd_kernel<%d>" % hd, fl):
-                L.check(L.lib().sca_attn_fwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal),
-                                             int(plus_one), L.stream_handle()), "sca_attn_fwd")
-        ctx.G, ctx.H, ctx.causal, ctx.plus_one = G, H, causal, plus_one
-        ctx.save_for_backward(key_valid, add_mask, *q, *k, *v, *o, *sm, *sl)
-        return tuple(o)
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, *ts):
+        cross = kind == "cross"
+        causal = kind == "causal"
+        xq = _contig(ts[:G])
+        o_ = G
+        xkv = _contig(ts[o_:o_ + G]) if cross else xq
+        o_ += G if cross else 0
+        W = ts[o_:o_ + 6 * G]
+        Wo, bo = ts[o_ + 6 * G:o_ + 7 * G], ts[o_ + 7 * G:o_ + 8 * G]
+        L.require_device(*xq, *xkv)
+        B, T, d = xq[0].shape
+        Tk = xkv[0].shape[1]
+        av = 0.5 if cross else 1.0
+        q, k, v, probs = [], [], [], []
+        for g in range(G):
+            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
+            xf, kf = _flat(xq[g]), _flat(xkv[g])
+            q.append(xq[g].new_empty(B, T, d))
+            k.append(xq[g].new_empty(B, Tk, d))
+            v.append(xq[g].new_empty(B, Tk, d))
+            probs.append(_prob([_seg(xf, Wq, d, d, d)], q[g], B * T, d, d, bias=bq, post_scale=scale))
+            probs.append(_prob([_seg(kf, Wk, d, d, d)], k[g], B * Tk, d, d, bias=bk))
+            probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
+        gemm(L.GEMM_NT, probs)
+        o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v)
+        ys = [torch.empty_like(x) for x in xq]
+        gemm(L.GEMM_NT, [_prob([_seg(_flat(o[g]), Wo[g], d, d, d)], ys[g], B * T, d, d, bias=bo[g],
+                               resid=_flat(xq[g]) if has_resid else None, ldr=d) for g in range(G)])
+        ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
+        ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
+                              *sm, *sl)
+        return tuple(ys)
 
     @staticmethod
-    def backward(ctx, *dout):
-        G, H = ctx.G, ctx.H
+    def backward(ctx, *dys):
+        G, kind, H, scale = ctx.G, ctx.kind, ctx.H, ctx.scale
+        cross = kind == "cross"
         sv = ctx.saved_tensors
         key_valid, add_mask = sv[0], sv[1]
-        q, k, v, o, sm, sl = (sv[2 + i * G:2 + (i + 1) * G] for i in range(6))
-        dout = _contig(_zeros_for_none(dout, o))
-        B, Tq, d = q[0].shape
-        Tk = k[0].shape[1]
-        hd = d // H
-        dq = [torch.empty_like(t) for t in q]
-        dk = [torch.empty_like(t) for t in k]
-        dv = [torch.empty_like(t) for t in v]
-        delta = [q[0].new_empty(B * H * Tq) for _ in range(G)]
-        for c in range(0, G, L.ATTN_MAX_PROBLEMS):
-            gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
-            arr = (L.AttnBwdProblem * len(gs))(*[
-                L.AttnBwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
-                                 dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
-                                 ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
-                                 delta[g].data_ptr(), 1.0, 1.0) for g in gs])
-            fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if ctx.causal else Tq * Tk)
-            with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
-                L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(ctx.causal),
-                                             int(ctx.plus_one), L.stream_handle()), "sca_attn_bwd")
-        return (None,) * 6 + tuple(dq) + tuple(dk) + tuple(dv)
+        i = 2
+        xq = sv[i:i + G]
+        i += G
+        xkv = sv[i:i + G] if cross else xq
+        i += G if cross else 0
+        W = sv[i:i + 6 * G]
+        i += 6 * G
+        Wo, bo = sv[i:i + G], sv[i + G:i + 2 * G]
+        i += 2 * G
+        q, k, v, o, sm, sl = (sv[i + j * G:i + (j + 1) * G] for j in range(6))
+        B, T, d = xq[0].shape
+        Tk = xkv[0].shape[1]
+        av = 0.5 if cross else 1.0
+        dys = _contig(_zeros_for_none(dys, xq))
+        # out-projection: dO = dY Wo
+        do = [torch.empty_like(t) for t in o]
+        gemm(L.GEMM_NN, [_prob([_seg(_flat(dys[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
+        dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do)
+        # input gradients (residual gradient fused as the epilogue's resid term)
+        dxq, dxkv, probs = [], [], []
+        for g in range(G):
+            Wq, _, Wk, _, Wv, _ = W[6 * g:6 * g + 6]
+            dqf, dkf, dvf = _flat(dq[g]), _flat(dk[g]), _flat(dv[g])
+            r = _flat(dys[g]) if ctx.has_resid else None
+            gx = torch.empty_like(xq[g])
+            if cross:
+                gkv = torch.empty_like(xkv[g])
+                probs.append(_prob([_seg(dqf, Wq, d, d, d, scale)], gx, B * T, d, d, resid=r, ldr=d))
+                probs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d, av)], gkv, B * Tk, d, d))
+                dxkv.append(gkv)
+            else:
+                probs.append(_prob([_seg(dqf, Wq, d, d, d, scale), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
+                                   gx, B * T, d, d, resid=r, ldr=d))
+            dxq.append(gx)
+        gemm(L.GEMM_NN, probs)
+        # weight / bias gradients (bias colsum fused in the TN GEMMs)
+        items = []
+        for g in range(G):
+            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
+            xf, kf = _flat(xq[g]), _flat(xkv[g])
+            items += [(_flat(dq[g]), xf, scale, Wq, bq is not None), (_flat(dk[g]), kf, 1.0, Wk, bk is not None),
+                      (_flat(dv[g]), kf, av, Wv, bv is not None, 1.0),
+                      (_flat(dys[g]), _flat(o[g]), 1.0, Wo[g], bo[g] is not None)]
+        wg = weight_grads(items)
+        dW, dWo, dbo = [], [], []
+        for g in range(G):
+            for j in range(3):
+                dW += list(wg[4 * g + j])
+            dWo.append(wg[4 * g + 3][0])
+            dbo.append(wg[4 * g + 3][1])
+        return (None,) * 8 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + tuple(dbo)
 
 
 # --------------------------------------------------------------------------- Linear (+ residual)
