@@ -87,6 +87,10 @@ typedef struct {
 int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
              void* stream);
 
+/* Tuning knob: force the workgroup tile of one layout (0 = built-in heuristic,
+ * 1 = 64x64, 2 = 128x64, 3 = 64x128, 4 = 128x128).  Process-global; not thread-safe.   */
+int sca_gemm_tile_override(int layout, int tile);
+
 /* Fused masked attention over (B, T, H*hd) row-major activations (head h at columns
  * h*hd .. h*hd+hd-1, row stride ld*).  Scores use q as given (the projection already
  * applied hd^-0.5).  Masking, per query row i and key j:

@@ -24,8 +24,7 @@
 
 namespace {
 
-constexpr int BK = 32;
-constexpr int KC_STRIDE = BK + 4;  // k-contiguous image row stride (floats)
+constexpr int KPAD = 4;  // LDS row padding (floats)
 
 struct GemmArgs {
   sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
@@ -33,23 +32,31 @@ struct GemmArgs {
   float* ws;
 };
 
-template <bool KCONTIG, int ROWS>
+// Workgroup tile configuration.
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int STAGES_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_, STAGES = STAGES_;
+  static constexpr int NT = 64 * WM * WN;             // threads
+  static constexpr int TM = BM / WM, TN = BN / WN;     // wave tile
+  static constexpr int RM = TM / 32, RN = TN / 32;     // 32x32 MFMA blocks per wave
+  static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32");
+};
+
+template <bool KCONTIG, int ROWS, int BK, int NT>
 struct Operand {
-  // LDS footprint in floats
-  static constexpr int kLds = KCONTIG ? ROWS * KC_STRIDE : BK * (ROWS + 4);
-  // float4 per thread for one BK slice of the tile
-  static constexpr int kVec = ROWS * BK / 4 / 256;
+  static constexpr int kLds = KCONTIG ? ROWS * (BK + KPAD) : BK * (ROWS + KPAD);  // floats
+  static constexpr int kVec = ROWS * BK / 4 / NT;  // float4 per thread per K-slice
+  static_assert(kVec >= 1 && ROWS * BK / 4 == kVec * NT, "tile not divisible among threads");
 };
 
 // Load one BK-slice of an operand tile from global into registers (zero outside bounds).
 // KCONTIG: global element (row, k) at base[row * ld + k];  else at base[k * ld + row].
-template <bool KCONTIG, int ROWS>
-__device__ __forceinline__ void load_tile(f32x4* reg, const float* base, int ld,
-                                          int row0, int nrows, int k0, int kend, float alpha) {
-  const int t = threadIdx.x;
+template <bool KCONTIG, int ROWS, int BK, int NT>
+__device__ __forceinline__ void load_tile(f32x4* reg, const float* base, int ld, int row0, int nrows, int k0,
+                                          int kend) {
 #pragma unroll
-  for (int i = 0; i < Operand<KCONTIG, ROWS>::kVec; ++i) {
-    const int e = t + i * 256;  // float4 index within the tile
+  for (int i = 0; i < Operand<KCONTIG, ROWS, BK, NT>::kVec; ++i) {
+    const int e = threadIdx.x + i * NT;  // float4 index within the tile
     int row, k;
     if (KCONTIG) {
       row = e / (BK / 4);
@@ -62,50 +69,47 @@ __device__ __forceinline__ void load_tile(f32x4* reg, const float* base, int ld,
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (KCONTIG) {
       if (gr < nrows && gk < kend) v = ld4(base + (long)gr * ld + gk);
-    } else {
-      if (gk < kend) {
-        if (gr + 3 < nrows) {
-          v = ld4(base + (long)gk * ld + gr);
-        } else {
+    } else if (gk < kend) {
+      if (gr + 3 < nrows) {
+        v = ld4(base + (long)gk * ld + gr);
+      } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (gr + j < nrows) v[j] = base[(long)gk * ld + gr + j];
-        }
+        for (int j = 0; j < 4; ++j)
+          if (gr + j < nrows) v[j] = base[(long)gk * ld + gr + j];
       }
     }
-    reg[i] = v * alpha;
+    reg[i] = v;
   }
 }
 
-template <bool KCONTIG, int ROWS>
-__device__ __forceinline__ void store_tile(float* lds, const f32x4* reg) {
-  const int t = threadIdx.x;
+// alpha is applied here, not at load time: a multiply right after the global load would
+// make the wave wait for the prefetch before the MFMAs it is meant to overlap.
+template <bool KCONTIG, int ROWS, int BK, int NT>
+__device__ __forceinline__ void store_tile(float* lds, const f32x4* reg, float alpha) {
 #pragma unroll
-  for (int i = 0; i < Operand<KCONTIG, ROWS>::kVec; ++i) {
-    const int e = t + i * 256;
+  for (int i = 0; i < Operand<KCONTIG, ROWS, BK, NT>::kVec; ++i) {
+    const int e = threadIdx.x + i * NT;
+    const f32x4 v = reg[i] * alpha;
     if (KCONTIG) {
       const int row = e / (BK / 4), k = (e % (BK / 4)) * 4;
-      st4(lds + row * KC_STRIDE + k, reg[i]);
+      st4(lds + row * (BK + KPAD) + k, v);
     } else {
       const int k = e / (ROWS / 4), row = (e % (ROWS / 4)) * 4;
-      st4(lds + k * (ROWS + 4) + row, reg[i]);
+      st4(lds + k * (ROWS + KPAD) + row, v);
     }
   }
 }
 
 // Fragment for k-group g8 (8 k values), block row offset r0 within the tile.
-template <bool KCONTIG, int ROWS>
+template <bool KCONTIG, int ROWS, int BK>
 __device__ __forceinline__ f32x4 read_frag(const float* lds, int r0, int g8, int lane) {
   const int r = r0 + (lane & 31);
   const int kb = g8 * 8 + (lane >> 5) * 4;
-  if (KCONTIG) {
-    return ld4(lds + r * KC_STRIDE + kb);
-  } else {
-    f32x4 v;
+  if (KCONTIG) return ld4(lds + r * (BK + KPAD) + kb);
+  f32x4 v;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) v[s] = lds[(kb + s) * (ROWS + 4) + r];
-    return v;
-  }
+  for (int s = 0; s < 4; ++s) v[s] = lds[(kb + s) * (ROWS + KPAD) + r];
+  return v;
 }
 
 __device__ __forceinline__ float epilogue(const sca_gemm_problem& P, int m, int n, float v) {
@@ -121,26 +125,35 @@ __device__ __forceinline__ float epilogue(const sca_gemm_problem& P, int m, int 
   return v;
 }
 
-template <int LAYOUT, int BM, int BN>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
+template <int LAYOUT, class C>
+__global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NT = C::NT, RM = C::RM, RN = C::RN;
   constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
   constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
-  using OpA = Operand<A_KC, BM>;
-  using OpB = Operand<B_KC, BN>;
-  constexpr int RM = BM / 64, RN = BN / 64;  // 32x32 blocks per wave
-  __shared__ __attribute__((aligned(16))) float smem[OpA::kLds + OpB::kLds];
-  float* As = smem;
-  float* Bs = smem + OpA::kLds;
+  using OpA = Operand<A_KC, BM, BK, NT>;
+  using OpB = Operand<B_KC, BN, BK, NT>;
+  constexpr int STAGE = OpA::kLds + OpB::kLds;
+  __shared__ __attribute__((aligned(16))) float smem[C::STAGES * STAGE];
+
+  // XCD-aware remap (cdna_hip_programming.md T1): hardware deals workgroups round-robin over
+  // the 8 XCDs; give each XCD a contiguous range of logical tiles (n fastest, then m, then
+  // problem / K-split) so tiles sharing an A row-block or a B column-block share one L2.
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
 
   const int splitk = args.splitk;
-  const int pid = blockIdx.z / splitk;
-  const int ks = blockIdx.z % splitk;
+  const int pid = bz / splitk;
+  const int ks = bz % splitk;
   const sca_gemm_problem& P = args.p[pid];
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = by * BM, n0 = bx * BN;
   if (m0 >= P.M || n0 >= P.N) return;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+  const int wm = (wave / C::WN) * C::TM, wn = (wave % C::WN) * C::TN;
 
   f32x16 acc[RM][RN];
 #pragma unroll
@@ -152,47 +165,86 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
 
   f32x4 ra[OpA::kVec], rb[OpB::kVec];
   // fused bias gradient (TN): the first column tile sums its A slices (= alpha * dY rows)
-  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && blockIdx.x == 0;
+  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && bx == 0;
   float bsum = 0.f;
 
-  for (int sidx = 0; sidx < P.nseg; ++sidx) {
-    const sca_gemm_seg S = P.seg[sidx];
-    int kbeg = 0, kend = S.K;
-    if (splitk > 1) {
-      const int chunk = ((S.K + splitk - 1) / splitk + BK - 1) / BK * BK;
-      kbeg = ks * chunk;
-      kend = min(S.K, kbeg + chunk);
+  // flatten (segment, K-slice) into one sequence so the pipeline runs across segments
+  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_kend[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
+    seg_kbeg[s] = seg_kend[s] = seg_n[s] = 0;
+    if (s < P.nseg) {
+      int kbeg = 0, kend = P.seg[s].K;
+      if (splitk > 1) {
+        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + BK - 1) / BK * BK;
+        kbeg = ks * chunk;
+        kend = min(P.seg[s].K, kbeg + chunk);
+      }
+      seg_kbeg[s] = kbeg;
+      seg_kend[s] = kend;
+      seg_n[s] = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+      total += seg_n[s];
     }
-    if (kbeg >= kend) continue;
-    load_tile<A_KC, BM>(ra, S.A, S.lda, m0, P.M, kbeg, kend, S.alpha);
-    load_tile<B_KC, BN>(rb, S.B, S.ldb, n0, P.N, kbeg, kend, 1.0f);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-      __syncthreads();
-      store_tile<A_KC, BM>(As, ra);
-      store_tile<B_KC, BN>(Bs, rb);
-      __syncthreads();
-      if (k0 + BK < kend) {
-        load_tile<A_KC, BM>(ra, S.A, S.lda, m0, P.M, k0 + BK, kend, S.alpha);
-        load_tile<B_KC, BN>(rb, S.B, S.ldb, n0, P.N, k0 + BK, kend, 1.0f);
-      }
-      if (do_bias && threadIdx.x < BM) {
+  }
+  float alpha_f = 1.f;  // alpha of the segment held in ra
+  auto fetch = [&](int t) {
+    int s = 0;
+    while (s + 1 < P.nseg && t >= seg_n[s]) { t -= seg_n[s]; ++s; }
+    const sca_gemm_seg& S = P.seg[s];
+    const int k0 = seg_kbeg[s] + t * BK;
+    load_tile<A_KC, BM, BK, NT>(ra, S.A, S.lda, m0, P.M, k0, seg_kend[s]);
+    load_tile<B_KC, BN, BK, NT>(rb, S.B, S.ldb, n0, P.N, k0, seg_kend[s]);
+    alpha_f = S.alpha;
+  };
+  auto compute = [&](const float* As, const float* Bs) {
+    if (do_bias && threadIdx.x < BM) {
 #pragma unroll 8
-        for (int k = 0; k < BK; ++k) bsum += As[k * (BM + 4) + threadIdx.x];  // TN: A image is [BK][BM+4]
+      for (int k = 0; k < BK; ++k) bsum += As[k * (BM + KPAD) + threadIdx.x];  // TN: A image is [BK][BM+4]
+    }
+#pragma unroll
+    for (int g8 = 0; g8 < BK / 8; ++g8) {
+      f32x4 fa[RM], fb[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) fa[i] = read_frag<A_KC, BM, BK>(As, wm + i * 32, g8, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) fb[j] = read_frag<B_KC, BN, BK>(Bs, wn + j * 32, g8, lane);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) acc[i][j] = mfma32(fa[i][s], fb[j][s], acc[i][j]);
+    }
+  };
+
+  if (C::STAGES == 1) {
+    if (total > 0) fetch(0);
+    for (int t = 0; t < total; ++t) {
+      __syncthreads();
+      store_tile<A_KC, BM, BK, NT>(smem, ra, alpha_f);
+      store_tile<B_KC, BN, BK, NT>(smem + OpA::kLds, rb, 1.0f);
+      __syncthreads();
+      if (t + 1 < total) fetch(t + 1);
+      compute(smem, smem + OpA::kLds);
+    }
+  } else {
+    if (total > 0) {
+      fetch(0);
+      store_tile<A_KC, BM, BK, NT>(smem, ra, alpha_f);
+      store_tile<B_KC, BN, BK, NT>(smem + OpA::kLds, rb, 1.0f);
+      __syncthreads();
+    }
+    for (int t = 0; t < total; ++t) {
+      const float* As = smem + (t & 1) * STAGE;
+      if (t + 1 < total) fetch(t + 1);  // global loads in flight during the MFMAs below
+      compute(As, As + OpA::kLds);
+      if (t + 1 < total) {
+        float* An = smem + ((t + 1) & 1) * STAGE;
+        store_tile<A_KC, BM, BK, NT>(An, ra, alpha_f);
+        store_tile<B_KC, BN, BK, NT>(An + OpA::kLds, rb, 1.0f);
       }
-#pragma unroll
-      for (int g8 = 0; g8 < BK / 8; ++g8) {
-        f32x4 fa[RM], fb[RN];
-#pragma unroll
-        for (int i = 0; i < RM; ++i) fa[i] = read_frag<A_KC, BM>(As, wm + i * 32, g8, lane);
-#pragma unroll
-        for (int j = 0; j < RN; ++j) fb[j] = read_frag<B_KC, BN>(Bs, wn + j * 32, g8, lane);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int j = 0; j < RN; ++j) acc[i][j] = mfma32(fa[i][s], fb[j][s], acc[i][j]);
-      }
+      __syncthreads();
     }
   }
 
@@ -201,12 +253,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
   const int rowh = 4 * (lane >> 5);
   if (do_bias && threadIdx.x < BM && m0 + (int)threadIdx.x < P.M) {
     if (splitk > 1)
-      args.ws[(long)gridDim.z * P.M * P.N + (long)blockIdx.z * P.M + m0 + threadIdx.x] = bsum;
+      args.ws[(long)gridDim.z * P.M * P.N + (long)bz * P.M + m0 + threadIdx.x] = bsum;
     else
       P.bias_grad[m0 + threadIdx.x] = bsum * P.bias_grad_scale;
   }
   if (splitk > 1) {
-    float* slab = args.ws + (long)blockIdx.z * P.M * P.N;
+    float* slab = args.ws + (long)bz * P.M * P.N;
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -219,18 +271,39 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
         }
     return;
   }
+  // epilogue: all loads of a 32x32 block first (one wait), then compute + store
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j)
+    for (int j = 0; j < RN; ++j) {
+      const int n = n0 + wn + j * 32 + col;
+      const bool nok = n < P.N;
+      const float bias = (P.bias && nok) ? P.bias[n] : 0.f;
+      float ex[16], ax[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
-        const int n = n0 + wn + j * 32 + col;
-        if (m < P.M && n < P.N) P.C[(long)m * P.ldc + n] = epilogue(P, m, n, acc[i][j][r]);
+        const bool ok = nok && m < P.M;
+        float e = 0.f;
+        if (ok && P.resid) e += P.resid[(long)m * P.ldr + n];
+        if (ok && (P.epi & SCA_EPI_ACCUM)) e += P.C[(long)m * P.ldc + n];
+        ex[r] = e;
+        ax[r] = (ok && (P.epi & SCA_EPI_DGELU)) ? P.aux[(long)m * P.ldx + n] : 0.f;
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
+        if (!nok || m >= P.M) continue;
+        float v = (acc[i][j][r] + bias) * P.post_scale;
+        if (P.epi & SCA_EPI_GELU) {
+          P.aux_out[(long)m * P.ldo + n] = v;
+          v = gelu_erf(v);
+        }
+        if (P.epi & SCA_EPI_DGELU) v *= gelu_erf_grad(ax[r]);
+        P.C[(long)m * P.ldc + n] = v + ex[r];
+      }
+    }
 }
-
 // Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]); bias partials likewise.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args, int nprob) {
   const sca_gemm_problem& P = args.p[blockIdx.y];
@@ -253,14 +326,58 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args,
   P.C[(long)m * P.ldc + n] = epilogue(P, m, n, v);
 }
 
-template <int LAYOUT, int BM, int BN>
+template <int LAYOUT, class C>
 int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  dim3 grid((maxN + BN - 1) / BN, (maxM + BM - 1) / BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_kernel<LAYOUT, BM, BN>), grid, dim3(256), 0, st, a);
+  dim3 grid((maxN + C::BN - 1) / C::BN, (maxM + C::BM - 1) / C::BM, nprob * a.splitk);
+  hipLaunchKernelGGL((gemm_kernel<LAYOUT, C>), grid, dim3(C::NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
+// Tile configurations (index = sca_gemm_tile_override value)
+using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
+using T2 = Cfg<128, 64, 2, 2, 32, 2>;   // 4 waves, 64x32
+using T3 = Cfg<64, 128, 2, 2, 32, 2>;   // 4 waves, 32x64
+using T4 = Cfg<128, 128, 2, 2, 32, 2>;  // 4 waves, 64x64
+using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
+using T6 = Cfg<128, 128, 2, 4, 32, 2>;  // 8 waves, 64x32
+using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
+using T8 = Cfg<64, 64, 2, 2, 64, 2>;    // BK 64
+using T9 = Cfg<64, 64, 2, 2, 16, 2>;    // BK 16
+constexpr int kNumTiles = 9;
+
+template <int LAYOUT>
+int launch_tile(int tile, const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  switch (tile) {
+    case 1: return launch<LAYOUT, T1>(a, nprob, maxM, maxN, st);
+    case 2: return launch<LAYOUT, T2>(a, nprob, maxM, maxN, st);
+    case 3: return launch<LAYOUT, T3>(a, nprob, maxM, maxN, st);
+    case 4: return launch<LAYOUT, T4>(a, nprob, maxM, maxN, st);
+    case 5: return launch<LAYOUT, T5>(a, nprob, maxM, maxN, st);
+    case 6: return launch<LAYOUT, T6>(a, nprob, maxM, maxN, st);
+    case 7: return launch<LAYOUT, T7>(a, nprob, maxM, maxN, st);
+    case 8: return launch<LAYOUT, T8>(a, nprob, maxM, maxN, st);
+    default: return launch<LAYOUT, T9>(a, nprob, maxM, maxN, st);
+  }
+}
+
+int g_tile_override[3] = {0, 0, 0};
+
+// Tile heuristic (measured, tools/gemm_bench.py): at these small per-stream shapes the
+// 64x64 tile wins; see DESIGN.md.
+int pick_tile(int layout, long tiles64, int splitk) {
+  if (g_tile_override[layout]) return g_tile_override[layout];
+  (void)tiles64;
+  (void)splitk;
+  return 1;
+}
+
 }  // namespace
+
+extern "C" int sca_gemm_tile_override(int layout, int tile) {
+  if (layout < 0 || layout > 2 || tile < 0 || tile > kNumTiles) return SCA_ERR_ARG;
+  g_tile_override[layout] = tile;
+  return SCA_OK;
+}
 
 extern "C" void sca_set_error(const char* msg);
 
@@ -309,10 +426,13 @@ extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, in
   if (maxM == 0 || maxN == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;
+  long tiles64 = 0;
+  for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
+  const int tile = pick_tile(layout, tiles64, splitk);
   switch (layout) {
-    case SCA_GEMM_NT: rc = launch<SCA_GEMM_NT, 64, 64>(a, nprob, maxM, maxN, st); break;
-    case SCA_GEMM_NN: rc = launch<SCA_GEMM_NN, 64, 64>(a, nprob, maxM, maxN, st); break;
-    default: rc = launch<SCA_GEMM_TN, 64, 64>(a, nprob, maxM, maxN, st); break;
+    case SCA_GEMM_NT: rc = launch_tile<SCA_GEMM_NT>(tile, a, nprob, maxM, maxN, st); break;
+    case SCA_GEMM_NN: rc = launch_tile<SCA_GEMM_NN>(tile, a, nprob, maxM, maxN, st); break;
+    default: rc = launch_tile<SCA_GEMM_TN>(tile, a, nprob, maxM, maxN, st); break;
   }
   if (rc != SCA_OK) { sca_set_error("sca_gemm: launch failed"); return rc; }
   if (splitk > 1) {
