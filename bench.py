@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from scattennet_amd import ops, workloads as W  # noqa: E402
+from scattennet_amd.dp import GradAllReduce  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA == fp32 vector peak
 HBM_PEAK_GBS = 8000.0
@@ -43,39 +44,6 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
-
-
-class GradAllReduce:
-    """Data parallelism over RCCL: gradients are averaged across ranks with ONE coalesced
-    fp32 all-reduce per step (flat buffer; the 4-stream SCA has 25.8 M params = 103 MB).
-    The reference has no DP at all — this is the north-star's batch-sharded
-    data parallelism, oracle: the single-process gradient of the full batch."""
-
-    def __init__(self, params, world):
-        self.params = [p for p in params if p.requires_grad]
-        self.world = world
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.empty(n, device=self.params[0].device, dtype=torch.float32)
-
-    def __call__(self):
-        if self.world == 1:
-            return
-        o = 0
-        views = []
-        for p in self.params:
-            k = p.numel()
-            v = self.flat[o:o + k]
-            if p.grad is None:
-                v.zero_()
-            else:
-                v.copy_(p.grad.reshape(-1))
-            views.append((p, v))
-            o += k
-        dist.all_reduce(self.flat)
-        self.flat.mul_(1.0 / self.world)
-        for p, v in views:
-            if p.grad is not None:
-                p.grad.copy_(v.view_as(p.grad))
 
 
 def main():
