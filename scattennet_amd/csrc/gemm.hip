@@ -30,6 +30,9 @@ struct GemmArgs {
   sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
   int splitk;
   float* ws;
+  int nprob;                                    // persistent kernel only:
+  int tile_prefix[SCA_GEMM_MAX_PROBLEMS + 1];  // cumulative output tiles (x splitk) per problem
+  int tiles_n[SCA_GEMM_MAX_PROBLEMS];           // column tiles per problem
 };
 
 // Workgroup tile configuration.
@@ -123,6 +126,45 @@ __device__ __forceinline__ float epilogue(const sca_gemm_problem& P, int m, int 
   if (P.resid) v += P.resid[(long)m * P.ldr + n];
   if (P.epi & SCA_EPI_ACCUM) v += P.C[(long)m * P.ldc + n];
   return v;
+}
+
+// Non-split epilogue of one wave's (RM x RN) 32x32 blocks: all loads of a block first (one
+// wait), then compute + store.  Order: v = (acc + bias) * post_scale; GELU (keeps the
+// pre-activation) / GELU'; + (resid + C_old).
+template <int RM, int RN>
+__device__ __forceinline__ void epilogue_block(const sca_gemm_problem& P, const f32x16 (&acc)[RM][RN], int mb, int nb,
+                                               int col, int rowh) {
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = nb + j * 32 + col;
+      const bool nok = n < P.N;
+      const float bias = (P.bias && nok) ? P.bias[n] : 0.f;
+      float ex[16], ax[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
+        const bool ok = nok && m < P.M;
+        float e = 0.f;
+        if (ok && P.resid) e += P.resid[(long)m * P.ldr + n];
+        if (ok && (P.epi & SCA_EPI_ACCUM)) e += P.C[(long)m * P.ldc + n];
+        ex[r] = e;
+        ax[r] = (ok && (P.epi & SCA_EPI_DGELU)) ? P.aux[(long)m * P.ldx + n] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
+        if (!nok || m >= P.M) continue;
+        float v = (acc[i][j][r] + bias) * P.post_scale;
+        if (P.epi & SCA_EPI_GELU) {
+          P.aux_out[(long)m * P.ldo + n] = v;
+          v = gelu_erf(v);
+        }
+        if (P.epi & SCA_EPI_DGELU) v *= gelu_erf_grad(ax[r]);
+        P.C[(long)m * P.ldc + n] = v + ex[r];
+      }
+    }
 }
 
 template <int LAYOUT, class C>
@@ -271,39 +313,196 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
         }
     return;
   }
-  // epilogue: all loads of a 32x32 block first (one wait), then compute + store
+  epilogue_block<RM, RN>(P, acc, m0 + wm, n0 + wn, col, rowh);
+}
+// ------------------------------------------------------------------------------ persistent
+// One output tile of the persistent kernel: integers only (wave-uniform).  Pointers and
+// leading dimensions are re-read from the kernel arguments (scalar loads) at each fetch,
+// which happens right after a barrier when no LDS reads are outstanding.
+struct TileInfo {
+  int pid, m0, n0, bn, ks, nsl, M, N;
+  int kb0, kb1, kb2, ke0, ke1, ke2, ns0, ns1;
+};
+
+template <int BM, int BN, int BK>
+__device__ __forceinline__ void decode_tile(const GemmArgs& a, int t, TileInfo& ti) {
+  int p = 0;
+  while (p + 1 < a.nprob && t >= a.tile_prefix[p + 1]) ++p;
+  const sca_gemm_problem& P = a.p[p];
+  const int local = t - a.tile_prefix[p];
+  const int tn = a.tiles_n[p], tm = (P.M + BM - 1) / BM;
+  ti.pid = p;
+  ti.M = P.M;
+  ti.N = P.N;
+  ti.bn = local % tn;
+  ti.ks = local / (tn * tm);
+  ti.m0 = ((local / tn) % tm) * BM;
+  ti.n0 = ti.bn * BN;
+  int kb[3], ke[3], ns[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    kb[s] = ke[s] = ns[s] = 0;
+    if (s < P.nseg) {
+      const int K = P.seg[s].K;
+      int b = 0, e = K;
+      if (a.splitk > 1) {
+        const int chunk = ((K + a.splitk - 1) / a.splitk + BK - 1) / BK * BK;
+        b = ti.ks * chunk;
+        e = min(K, b + chunk);
+      }
+      kb[s] = b;
+      ke[s] = e;
+      ns[s] = e > b ? (e - b + BK - 1) / BK : 0;
+    }
+  }
+  ti.kb0 = kb[0]; ti.kb1 = kb[1]; ti.kb2 = kb[2];
+  ti.ke0 = ke[0]; ti.ke1 = ke[1]; ti.ke2 = ke[2];
+  ti.ns0 = ns[0]; ti.ns1 = ns[1];
+  ti.nsl = ns[0] + ns[1] + ns[2];
+}
+
+// Persistent grouped GEMM: each workgroup walks its share of ALL problems' output tiles and
+// the K-slices of consecutive tiles form one continuous double-buffered pipeline: the next
+// tile's first slice is fetched while the current tile finishes, so short-K tiles
+// (K = 256..768 here) pay no per-tile pipeline fill.
+template <int LAYOUT, class C>
+__global__ __launch_bounds__(C::NT) void gemm_persistent_kernel(const GemmArgs args) {
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NT = C::NT, RM = C::RM, RN = C::RN;
+  constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
+  constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
+  using OpA = Operand<A_KC, BM, BK, NT>;
+  using OpB = Operand<B_KC, BN, BK, NT>;
+  constexpr int STAGE = OpA::kLds + OpB::kLds;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const unsigned nwg = gridDim.x;
+  const unsigned orig = blockIdx.x;
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (int)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3));
+  const int total_tiles = args.tile_prefix[args.nprob];
+  if (wgid >= total_tiles) return;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave / C::WN) * C::TM, wn = (wave % C::WN) * C::TN;
+  const int col = lane & 31;
+  const int rowh = 4 * (lane >> 5);
+
+  f32x16 acc[RM][RN];
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int n = n0 + wn + j * 32 + col;
-      const bool nok = n < P.N;
-      const float bias = (P.bias && nok) ? P.bias[n] : 0.f;
-      float ex[16], ax[16];
+    for (int j = 0; j < RN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
-        const bool ok = nok && m < P.M;
-        float e = 0.f;
-        if (ok && P.resid) e += P.resid[(long)m * P.ldr + n];
-        if (ok && (P.epi & SCA_EPI_ACCUM)) e += P.C[(long)m * P.ldc + n];
-        ex[r] = e;
-        ax[r] = (ok && (P.epi & SCA_EPI_DGELU)) ? P.aux[(long)m * P.ldx + n] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
-        if (!nok || m >= P.M) continue;
-        float v = (acc[i][j][r] + bias) * P.post_scale;
-        if (P.epi & SCA_EPI_GELU) {
-          P.aux_out[(long)m * P.ldo + n] = v;
-          v = gelu_erf(v);
-        }
-        if (P.epi & SCA_EPI_DGELU) v *= gelu_erf_grad(ax[r]);
-        P.C[(long)m * P.ldc + n] = v + ex[r];
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  f32x4 ra[OpA::kVec], rb[OpB::kVec];
+  float alpha_f = 1.f;
+  auto fetch = [&](const TileInfo& ti, int sl) {
+    int s = 0, kb = ti.kb0, ke = ti.ke0;
+    if (sl >= ti.ns0) {
+      sl -= ti.ns0;
+      s = 1, kb = ti.kb1, ke = ti.ke1;
+      if (sl >= ti.ns1) {
+        sl -= ti.ns1;
+        s = 2, kb = ti.kb2, ke = ti.ke2;
       }
     }
+    const sca_gemm_seg& S = args.p[ti.pid].seg[s];
+    const int k0 = kb + sl * BK;
+    load_tile<A_KC, BM, BK, NT>(ra, S.A, S.lda, ti.m0, ti.M, k0, ke);
+    load_tile<B_KC, BN, BK, NT>(rb, S.B, S.ldb, ti.n0, ti.N, k0, ke);
+    alpha_f = S.alpha;
+  };
+
+  float bsum = 0.f;
+  TileInfo cur, nxt;
+  int t = wgid;
+  decode_tile<BM, BN, BK>(args, t, cur);
+  int sl = 0;
+  fetch(cur, 0);
+  store_tile<A_KC, BM, BK, NT>(smem, ra, alpha_f);
+  store_tile<B_KC, BN, BK, NT>(smem + OpA::kLds, rb, 1.0f);
+  __syncthreads();
+  int buf = 0;
+  while (true) {
+    bool have_next = true;
+    int nsl_idx = sl + 1;
+    int tn = t;
+    if (nsl_idx >= cur.nsl) {
+      nsl_idx = 0;
+      tn = t + (int)nwg;
+      have_next = tn < total_tiles;
+      if (have_next) decode_tile<BM, BN, BK>(args, tn, nxt);
+    } else {
+      nxt = cur;
+    }
+    if (have_next) fetch(nxt, nsl_idx);  // in flight during the MFMAs below
+
+    const float* As = smem + buf * STAGE;
+    const float* Bs = As + OpA::kLds;
+    const sca_gemm_problem& P = args.p[cur.pid];
+    const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && cur.bn == 0;
+    if (do_bias && threadIdx.x < BM) {
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) bsum += As[k * (BM + KPAD) + threadIdx.x];  // TN: A image is [BK][BM+4]
+    }
+#pragma unroll
+    for (int g8 = 0; g8 < BK / 8; ++g8) {
+      f32x4 fa[RM], fb[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) fa[i] = read_frag<A_KC, BM, BK>(As, wm + i * 32, g8, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) fb[j] = read_frag<B_KC, BN, BK>(Bs, wn + j * 32, g8, lane);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j) acc[i][j] = mfma32(fa[i][s], fb[j][s], acc[i][j]);
+    }
+    if (sl + 1 >= cur.nsl) {  // tile complete: epilogue (the next tile's loads stay in flight)
+      if (do_bias && threadIdx.x < BM && cur.m0 + (int)threadIdx.x < P.M) {
+        if (args.splitk > 1)
+          args.ws[(long)args.nprob * args.splitk * P.M * P.N + ((long)cur.pid * args.splitk + cur.ks) * P.M +
+                  cur.m0 + threadIdx.x] = bsum;
+        else
+          P.bias_grad[cur.m0 + threadIdx.x] = bsum * P.bias_grad_scale;
+      }
+      bsum = 0.f;
+      if (args.splitk > 1) {
+        float* slab = args.ws + ((long)cur.pid * args.splitk + cur.ks) * P.M * P.N;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int m = cur.m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
+              const int n = cur.n0 + wn + j * 32 + col;
+              if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[i][j][r];
+            }
+      } else {
+        epilogue_block<RM, RN>(P, acc, cur.m0 + wm, cur.n0 + wn, col, rowh);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
+    if (!have_next) break;
+    buf ^= 1;
+    float* An = smem + buf * STAGE;
+    store_tile<A_KC, BM, BK, NT>(An, ra, alpha_f);
+    store_tile<B_KC, BN, BK, NT>(An + OpA::kLds, rb, 1.0f);
+    __syncthreads();
+    cur = nxt;
+    sl = nsl_idx;
+    t = tn;
+  }
 }
+
 // Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]); bias partials likewise.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args, int nprob) {
   const sca_gemm_problem& P = args.p[blockIdx.y];
@@ -326,6 +525,39 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args,
   P.C[(long)m * P.ldc + n] = epilogue(P, m, n, v);
 }
 
+int pick_grid(int tiles, int max_per_cu) {
+  int best_w = 1;
+  long best = -1;
+  for (int w = 1; w <= max_per_cu; ++w) {
+    const long span = (long)((tiles + 256 * w - 1) / (256 * w)) * w;
+    if (best < 0 || span <= best) {
+      best = span;
+      best_w = w;
+    }
+  }
+  const int g = 256 * best_w;
+  return tiles < g ? tiles : g;
+}
+
+template <int LAYOUT, class C>
+int launch_persistent(GemmArgs& a, int nprob, hipStream_t st) {
+  a.nprob = nprob;
+  a.tile_prefix[0] = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const int tm = (a.p[i].M + C::BM - 1) / C::BM, tn = (a.p[i].N + C::BN - 1) / C::BN;
+    a.tiles_n[i] = tn;
+    a.tile_prefix[i + 1] = a.tile_prefix[i] + tm * tn * a.splitk;
+  }
+  const int tiles = a.tile_prefix[nprob];
+  if (tiles == 0) return SCA_OK;
+  constexpr int lds = 2 * (Operand<LAYOUT != SCA_GEMM_TN, C::BM, C::BK, C::NT>::kLds +
+                           Operand<LAYOUT == SCA_GEMM_NT, C::BN, C::BK, C::NT>::kLds) * 4;
+  int per_cu = (160 * 1024) / lds;
+  per_cu = per_cu < 4 ? (per_cu < 1 ? 1 : per_cu) : 4;
+  hipLaunchKernelGGL((gemm_persistent_kernel<LAYOUT, C>), dim3(pick_grid(tiles, per_cu)), dim3(C::NT), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
 template <int LAYOUT, class C>
 int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + C::BN - 1) / C::BN, (maxM + C::BM - 1) / C::BM, nprob * a.splitk);
@@ -345,9 +577,27 @@ using T8 = Cfg<64, 64, 2, 2, 64, 2>;    // BK 64
 using T9 = Cfg<64, 64, 2, 2, 16, 2>;    // BK 16
 constexpr int kNumTiles = 9;
 
+// persistent kernels need every tile to own >= 1 K-slice (no empty split-K chunks)
+bool persistent_ok(const GemmArgs& a, int nprob) {
+  for (int i = 0; i < nprob; ++i)
+    for (int s = 0; s < a.p[i].nseg; ++s) {
+      const int K = a.p[i].seg[s].K;
+      const int chunk = ((K + a.splitk - 1) / a.splitk + 31) / 32 * 32;
+      if (K < 1 || (a.splitk > 1 && (long)(a.splitk - 1) * chunk >= K)) return false;
+    }
+  return true;
+}
+
 template <int LAYOUT>
-int launch_tile(int tile, const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  if (tile > 10 && !persistent_ok(a, nprob)) tile = 1;
   switch (tile) {
+    case 11: return launch_persistent<LAYOUT, T1>(a, nprob, st);
+    case 12: return launch_persistent<LAYOUT, T2>(a, nprob, st);
+    case 13: return launch_persistent<LAYOUT, T3>(a, nprob, st);
+    case 14: return launch_persistent<LAYOUT, T4>(a, nprob, st);
+    case 15: return launch_persistent<LAYOUT, T6>(a, nprob, st);
+    case 16: return launch_persistent<LAYOUT, T7>(a, nprob, st);
     case 1: return launch<LAYOUT, T1>(a, nprob, maxM, maxN, st);
     case 2: return launch<LAYOUT, T2>(a, nprob, maxM, maxN, st);
     case 3: return launch<LAYOUT, T3>(a, nprob, maxM, maxN, st);
@@ -374,7 +624,7 @@ int pick_tile(int layout, long tiles64, int splitk) {
 }  // namespace
 
 extern "C" int sca_gemm_tile_override(int layout, int tile) {
-  if (layout < 0 || layout > 2 || tile < 0 || tile > kNumTiles) return SCA_ERR_ARG;
+  if (layout < 0 || layout > 2 || tile < 0 || (tile > kNumTiles && (tile < 11 || tile > 16))) return SCA_ERR_ARG;
   g_tile_override[layout] = tile;
   return SCA_OK;
 }

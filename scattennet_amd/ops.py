@@ -113,6 +113,42 @@ def _splitk_for(M_red, n_out_tiles):
     return sk
 
 
+# ---- weight-gradient side stream -------------------------------------------------------
+# The weight/bias-gradient GEMMs of a layer do not feed the rest of the backward pass, so
+# they run on a side HIP stream, concurrently with the input-gradient GEMMs and attention
+# backward of the same and the next layers (each launch alone fills the chip poorly at
+# these sizes).  A callback queued on the autograd engine joins the side stream into the
+# caller's stream when backward() completes, so .grad is safe to read afterwards exactly as
+# with a single stream (the same mechanism torch DDP uses).  Captured into hipGraphs as a
+# fork/join.  SCA_WGRAD_STREAM=0 disables it.
+import os as _os
+
+_WGRAD_SIDE = _os.environ.get("SCA_WGRAD_STREAM", "1") != "0"
+_side_streams = {}
+_join_pending = {}
+
+
+def _side_stream(device):
+    st = _side_streams.get(device)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _side_streams[device] = st
+    return st
+
+
+def _queue_join(main, side):
+    key = (main.cuda_stream, side.cuda_stream)
+    if _join_pending.get(key):
+        return
+    _join_pending[key] = True
+
+    def _join():
+        _join_pending[key] = False
+        main.wait_stream(side)
+
+    torch.autograd.Variable._execution_engine.queue_callback(_join)
+
+
 def weight_grads(items, M=None):
     """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
     the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
@@ -120,6 +156,22 @@ def weight_grads(items, M=None):
     items: list of (dY[M,out], X[M,in], alpha, W_like, has_bias[, bias_scale]) -> [(dW, db)].
     bias_scale defaults to alpha; it differs when alpha scales the INPUT X (v from kv/2:
     dWv = dV^T (kv/2) but dbv = colsum(dV))."""
+    if not _WGRAD_SIDE:
+        return _weight_grads(items)
+    dev = items[0][0].device
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)  # dY and X are ready on the main stream
+    for it in items:  # keep their memory from being reused by the main stream too early
+        it[0].record_stream(side)
+        it[1].record_stream(side)
+    with torch.cuda.stream(side):
+        out = _weight_grads(items)
+    _queue_join(main, side)
+    return out
+
+
+def _weight_grads(items):
     out = []
     by_shape = {}  # split-K needs equal problem shapes within a launch
     items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]

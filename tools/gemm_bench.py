@@ -13,7 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-TILES = {1: "64x64", 2: "128x64", 3: "64x128", 4: "128x128", 5: "128sq8w", 6: "128x64w8"}
+TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 9: "64bk16", 11: "P64x64", 12: "P128x64", 14: "P128sq", 15: "P128sq8w", 16: "P128x64w8"}
 
 
 def make_case(name, layout, shapes, splitk=1, segs=1):
