@@ -57,18 +57,23 @@ def main():
     dev = torch.device("cuda", local)
     w = W.WORKLOADS[args.workload]
 
-    model = W.build_streams(w, dev, seed=0, init="reference")
+    fusion = bool(w.get("fusion"))
+    model = W.build_encoder(w, dev, seed=0) if fusion else W.build_streams(w, dev, seed=0, init="reference")
     if world > 1:  # identical initial weights on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     kp, mask, gout = W.synthetic_batch(w, dev, seed=1 + rank)
-    grads_out = [gout[g].contiguous() for g in range(len(w["groups"]))]
+    grads_out = [gout[g].contiguous() for g in range(gout.shape[0])]
     allreduce = GradAllReduce(model.parameters(), world)
     params = [p for p in model.parameters()]
 
-    def step():
+    def fwd_bwd():
         outs = model(kp, mask)
+        outs = outs[:1] if fusion else outs  # config 3: the loss seed sits on the fusion output
         torch.autograd.backward(outs, grads_out)
+
+    def step():
+        fwd_bwd()
         allreduce()
 
     # warm-up (also builds the library's lazy state) on a side stream, as graph capture requires
@@ -82,21 +87,25 @@ def main():
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
 
+    # the captured graph holds forward + backward (~200 HIP launches); the RCCL gradient
+    # all-reduce (N > 1) runs eagerly right after each replay on the same stream
     graph = None
     if not args.no_graph:
         for p in params:
             p.grad = None
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            step()
+            fwd_bwd()
         for _ in range(2):
             graph.replay()
+            allreduce()
         torch.cuda.synchronize()
 
     def run(k):
         for _ in range(k):
             if graph is not None:
                 graph.replay()
+                allreduce()
             else:
                 for p in params:
                     p.grad = None
@@ -136,7 +145,7 @@ def main():
                 "step_frac": round(step_flops / (ms / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not fusion:
         cpu = cpu_baseline(w, model, args.cpu_seconds)
 
     if rank == 0:
@@ -158,6 +167,10 @@ def main():
 
 
 def describe(w):
+    if w.get("fusion"):
+        return (f"full encoder: {len(w['groups'])} streams (mapping + {w['L']}x SCA + residual "
+                f"{w['residual_blocks']}) + CoordinatesFusion {w['in_fusion']}->{w['out_fusion']}, "
+                f"B={w['B']} T={w['T']} K={w['K_all']} d={w['d']} H={w['H']}, fwd+bwd all params")
     return (f"{len(w['groups'])}-stream SCA (mapping + {w['L']}x self / causal / cross-merge), "
             f"B={w['B']} T={w['T']} K={w['K_all']} d={w['d']} H={w['H']}, fwd+bwd all params")
 

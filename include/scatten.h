@@ -22,6 +22,10 @@
  *   sca_coord_map_fwd/bwd  KeypointModule stream slicing + CoordinateMapping
  *                          (model/__init__.py:133-142, keypoint_module.py:22-26,
  *                          layers.py:111-123)
+ *   sca_maxpool_t_fwd/bwd  ResidualBlock MaxPool1d(2,2) over frames (residual.py:40-43)
+ *   sca_softmax_rows_*     CoordinatesFusion softmax (fusion.py:52-53)
+ *   sca_gelu_bwd           GELU backward where no GEMM epilogue can absorb it
+ *                          (fusion.py:43-50,74-77)
  */
 #ifndef SCATTEN_H
 #define SCATTEN_H
@@ -190,6 +194,29 @@ typedef struct {
 #define SCA_POOL_MAX_PROBLEMS 8
 int sca_maxpool_t_fwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream);
 int sca_maxpool_t_bwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream);
+
+/* Row softmax over the last dim (N <= 1024) and its backward (CoordinatesFusion's
+ * unscaled, unmasked attention weights, model/fusion.py:52-53):
+ *   fwd: y = softmax(x)            bwd: dx = y * (dy - sum_j dy_j y_j)                  */
+typedef struct {
+  const float* x;  /* fwd input */
+  const float* y;  /* fwd output / bwd input */
+  const float* dy;
+  float* out;      /* fwd: y ; bwd: dx */
+} sca_softmax_problem;
+#define SCA_SOFTMAX_MAX_PROBLEMS 8
+int sca_softmax_rows_fwd(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream);
+int sca_softmax_rows_bwd(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream);
+
+/* Elementwise GELU backward: dz = dy * gelu_erf'(z) over n elements (the pre-activation z
+ * is what the GEMM GELU epilogue stored).                                               */
+typedef struct {
+  const float* dy;
+  const float* z;
+  float* dz;
+} sca_gelu_bwd_problem;
+#define SCA_GELU_MAX_PROBLEMS 8
+int sca_gelu_bwd(int nprob, const sca_gelu_bwd_problem* probs, long n, void* stream);
 
 /* out[i, j] (+)= scale * sum_{s < S} in[s * stride_s + i * stride_i + j],  i < I, j < N.
  * Column sums (bias gradients), slab reductions, position-table gradients.            */

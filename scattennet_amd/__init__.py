@@ -5,6 +5,8 @@ model/keypoint_module.py, model/fusion.py and their helpers).
 Drop-in modules keep the reference constructors, forward signatures and state_dict keys;
 their math runs in hand-written HIP kernels (libscatten_hip.so, C ABI in include/scatten.h).
 """
+from .encoder import SCAEncoder  # noqa: F401
+from .fusion import CoordinatesFusion, InvertedResidual  # noqa: F401
 from .attention import BaseAttention, CrossAttention, SelfAttention, SelfCausalAttention  # noqa: F401
 from .keypoint_module import (CoordinateAttention, CoordinatesMerge, KeypointModule, KeypointStreams,  # noqa: F401
                               SeparativeCoordinateAttention)

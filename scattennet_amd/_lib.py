@@ -22,6 +22,8 @@ LN_MAX_PROBLEMS = 8
 REDUCE_MAX_PROBLEMS = 16
 MAP_MAX_PROBLEMS = 8
 POOL_MAX_PROBLEMS = 8
+SOFTMAX_MAX_PROBLEMS = 8
+GELU_MAX_PROBLEMS = 8
 ACT_NONE, ACT_RELU = 0, 1
 
 
@@ -63,6 +65,14 @@ class PoolProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("dy", c_void_p), ("dx", c_void_p)]
 
 
+class SoftmaxProblem(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("dy", c_void_p), ("out", c_void_p)]
+
+
+class GeluBwdProblem(ctypes.Structure):
+    _fields_ = [("dy", c_void_p), ("z", c_void_p), ("dz", c_void_p)]
+
+
 class ReduceProblem(ctypes.Structure):
     _fields_ = [("inp", c_void_p), ("out", c_void_p), ("scale", c_float)]
 
@@ -88,6 +98,9 @@ EXPORTS = {
     "sca_layernorm_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p], c_int),
     "sca_maxpool_t_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_maxpool_t_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_softmax_rows_fwd": ([c_int, c_void_p, c_int, c_int, c_void_p], c_int),
+    "sca_softmax_rows_bwd": ([c_int, c_void_p, c_int, c_int, c_void_p], c_int),
+    "sca_gelu_bwd": ([c_int, c_void_p, c_long, c_void_p], c_int),
     "sca_reduce_rows": ([c_int, c_void_p, c_int, c_int, c_int, c_long, c_long, c_int, c_void_p], c_int),
     "sca_coord_map_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_coord_map_bwd_chunks": ([c_int], c_int),

@@ -233,6 +233,82 @@ int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
+// ------------------------------------------------------------------------------ row softmax
+struct SoftmaxArgs {
+  sca_softmax_problem p[SCA_SOFTMAX_MAX_PROBLEMS];
+  int rows, N;
+};
+
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const SoftmaxArgs a) {
+  using RM = RowMap<NV>;
+  constexpr int V = RM::kVals;
+  const sca_softmax_problem& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int N = a.N;
+  float v[V];
+  load_row<NV>(v, P.x + (long)row * N, lane, N);
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+    if (NV > 0 || RM::col(lane, i) < N) m = fmaxf(m, v[i]);
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const bool in = NV > 0 || RM::col(lane, i) < N;
+    v[i] = in ? __expf(v[i] - m) : 0.f;
+    s += v[i];
+  }
+  const float inv = 1.0f / wave_sum(s);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] *= inv;
+  store_row<NV>(P.out + (long)row * N, v, lane, N);
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const SoftmaxArgs a) {
+  using RM = RowMap<NV>;
+  constexpr int V = RM::kVals;
+  const sca_softmax_problem& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int N = a.N;
+  float y[V], g[V];
+  load_row<NV>(y, P.y + (long)row * N, lane, N);
+  load_row<NV>(g, P.dy + (long)row * N, lane, N);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) s += y[i] * g[i];
+  s = wave_sum(s);
+#pragma unroll
+  for (int i = 0; i < V; ++i) g[i] = y[i] * (g[i] - s);
+  store_row<NV>(P.out + (long)row * N, g, lane, N);
+}
+
+// ------------------------------------------------------------------------------ GELU backward
+struct GeluArgs {
+  sca_gelu_bwd_problem p[SCA_GELU_MAX_PROBLEMS];
+  long n;
+};
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const GeluArgs a) {
+  const sca_gelu_bwd_problem& P = a.p[blockIdx.y];
+  const long n4 = a.n / 4;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n4; e += (long)gridDim.x * 256) {
+    const f32x4 dy = ld4(P.dy + 4 * e), z = ld4(P.z + 4 * e);
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = dy[j] * gelu_erf_grad(z[j]);
+    st4(P.dz + 4 * e, r);
+  }
+  for (long e = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; e < a.n; e += (long)gridDim.x * 256)
+    P.dz[e] = P.dy[e] * gelu_erf_grad(P.z[e]);
+}
+
 // ------------------------------------------------------------------------------ MaxPool1d(2,2) over T
 struct PoolArgs {
   sca_pool_problem p[SCA_POOL_MAX_PROBLEMS];
@@ -454,6 +530,66 @@ extern "C" int sca_maxpool_t_bwd(int nprob, const sca_pool_problem* probs, int B
   const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
   hipLaunchKernelGGL(maxpool_t_bwd_kernel, dim3(blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_maxpool_t_bwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+template <bool BWD>
+int launch_softmax(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream, const char* what) {
+  if (nprob < 1 || nprob > SCA_SOFTMAX_MAX_PROBLEMS || rows < 0 || N < 1 || N > 64 * LN_MAXV) {
+    sca_set_error(what);
+    return SCA_ERR_ARG;
+  }
+  if (rows == 0) return SCA_OK;
+  SoftmaxArgs a;
+  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  a.rows = rows;
+  a.N = N;
+  dim3 grid((rows + 3) / 4, nprob);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nv = N % 256 == 0 ? N / 256 : 0;
+#define SCA_SM(NVV)                                                                   \
+  if (BWD) hipLaunchKernelGGL(softmax_bwd_kernel<NVV>, grid, dim3(256), 0, st, a);   \
+  else hipLaunchKernelGGL(softmax_fwd_kernel<NVV>, grid, dim3(256), 0, st, a);
+  switch (nv) {
+    case 1: SCA_SM(1) break;
+    case 2: SCA_SM(2) break;
+    case 3: SCA_SM(3) break;
+    case 4: SCA_SM(4) break;
+    default: SCA_SM(0) break;
+  }
+#undef SCA_SM
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_softmax_rows: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_softmax_rows_fwd(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream) {
+  return launch_softmax<false>(nprob, probs, rows, N, stream, "sca_softmax_rows_fwd: bad arguments (N <= 1024)");
+}
+
+extern "C" int sca_softmax_rows_bwd(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream) {
+  return launch_softmax<true>(nprob, probs, rows, N, stream, "sca_softmax_rows_bwd: bad arguments (N <= 1024)");
+}
+
+extern "C" int sca_gelu_bwd(int nprob, const sca_gelu_bwd_problem* probs, long n, void* stream) {
+  if (nprob < 1 || nprob > SCA_GELU_MAX_PROBLEMS || n < 0) {
+    sca_set_error("sca_gelu_bwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  if (n == 0) return SCA_OK;
+  GeluArgs a;
+  for (int i = 0; i < nprob; ++i) {
+    a.p[i] = probs[i];
+    if ((reinterpret_cast<uintptr_t>(probs[i].dy) | reinterpret_cast<uintptr_t>(probs[i].z) |
+         reinterpret_cast<uintptr_t>(probs[i].dz)) & 15) {
+      sca_set_error("sca_gelu_bwd: pointers must be 16-byte aligned");
+      return SCA_ERR_ARG;
+    }
+  }
+  a.n = n;
+  const long blocks = (n / 4 + 255) / 256;
+  dim3 grid((unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048), nprob);
+  hipLaunchKernelGGL(gelu_bwd_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gelu_bwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
 

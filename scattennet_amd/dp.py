@@ -17,6 +17,11 @@ import torch.distributed as dist
 
 
 class GradAllReduce:
+    """Average the gradients of `params` over all ranks with one coalesced all-reduce.
+
+    Flatten (one cat launch), all-reduce, scatter back (one multi-tensor copy launch); the
+    set of parameters holding a gradient is structural (identical on every rank)."""
+
     def __init__(self, params, world=None, average=True):
         self.params = [p for p in params if p.requires_grad]
         self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
@@ -27,20 +32,17 @@ class GradAllReduce:
     def __call__(self):
         if self.world == 1:
             return
-        o = 0
-        views = []
-        for p in self.params:
-            k = p.numel()
-            v = self.flat[o:o + k]
-            if p.grad is None:
-                v.zero_()
-            else:
-                v.copy_(p.grad.reshape(-1))
-            views.append((p, v))
-            o += k
-        dist.all_reduce(self.flat)
+        grads = [p.grad for p in self.params if p.grad is not None]
+        if not grads:
+            return
+        n = sum(g.numel() for g in grads)
+        flat = self.flat[:n]
+        torch.cat([g.reshape(-1) for g in grads], out=flat)
+        dist.all_reduce(flat)
         if self.average:
-            self.flat.mul_(1.0 / self.world)
-        for p, v in views:
-            if p.grad is not None:
-                p.grad.copy_(v.view_as(p.grad))
+            flat.mul_(1.0 / self.world)
+        views, o = [], 0
+        for g in grads:
+            views.append(flat[o:o + g.numel()].view_as(g))
+            o += g.numel()
+        torch._foreach_copy_(grads, views)

@@ -1,0 +1,65 @@
+"""Drop-in CoordinatesFusion + InvertedResidual (model/fusion.py of tinh2044/SCAttenNet):
+the cross-stream fusion of the left / right / body stream encodings (BASELINE config 3)."""
+import torch.nn as nn
+
+from . import ops
+from .layers import layernorm_grouped
+
+
+def _lin(layers, xs, gelu=False, resid=None):
+    G = len(xs)
+    W = [l.weight for l in layers]
+    b = [l.bias for l in layers]
+    extra = list(resid) if resid is not None else []
+    if gelu:
+        return list(ops.LinearGelu.apply(G, resid is not None, *xs, *W, *b, *extra))
+    return list(ops.LinearResidual.apply(G, resid is not None, *xs, *W, *b, *extra))
+
+
+class CoordinatesFusion(nn.Module):
+    """model/fusion.py:6-55.
+
+    l, r, b = GELU(Linear_in->out(.)) (one grouped launch); A = softmax(r l^T) per clip —
+    no 1/sqrt(d) scale and no mask, so padded frames take part, as in the reference;
+    f = LayerNorm(out_proj(A b)); out = InvertedResidual(f)."""
+
+    def __init__(self, in_feat, out_feat, drop_rate=0.0):
+        super().__init__()
+        self.left_se = nn.Linear(in_feat, out_feat)
+        self.right_se = nn.Linear(in_feat, out_feat)
+        self.body_se = nn.Linear(in_feat, out_feat)
+        self.out_proj = nn.Linear(out_feat, out_feat)
+        self.norm = nn.LayerNorm(out_feat)
+        self.gelu = nn.GELU()
+        self.inverted_res = InvertedResidual(out_feat, out_feat)
+        self.drop_rate = drop_rate
+
+    def forward(self, left_embed, right_embed, body_embed):
+        if self.training and self.drop_rate > 0:
+            raise NotImplementedError("CoordinatesFusion dropout > 0 in training mode is not implemented "
+                                      "(use eval() or drop_rate=0)")
+        lo, ro, bo = _lin([self.left_se, self.right_se, self.body_se], [left_embed, right_embed, body_embed],
+                          gelu=True)
+        attn = ops.SoftmaxRows.apply(ops.ClipMatmul.apply(True, ro, lo))
+        fuse = ops.ClipMatmul.apply(False, attn, bo)
+        fuse = _lin([self.out_proj], [fuse])
+        fuse = layernorm_grouped([self.norm], fuse)[0]
+        return self.inverted_res(fuse)
+
+
+class InvertedResidual(nn.Module):
+    """model/fusion.py:58-78: LN(GELU(L1 x) + x) -> GELU(L2 .) -> L3 (no outer residual)."""
+
+    def __init__(self, in_dim, out_dim):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_dim, in_dim)
+        self.linear_2 = nn.Linear(in_dim, in_dim * 3)
+        self.linear_3 = nn.Linear(in_dim * 3, out_dim)
+        self.gelu = nn.GELU()
+        self.bn1 = nn.LayerNorm(in_dim)
+
+    def forward(self, x):
+        out = _lin([self.linear_1], [x], gelu=True, resid=[x])
+        out = layernorm_grouped([self.bn1], out)
+        out = _lin([self.linear_2], out, gelu=True)
+        return _lin([self.linear_3], out)[0]

@@ -168,14 +168,22 @@ class KeypointStreams(nn.Module):
 
     def joint_indices(self, device):
         if self._idx is None or self._idx[0].device != device:
-            self._idx = [torch.tensor(list(m.joint_idx), dtype=torch.int32, device=device) for m in self.streams]
+            self._idx = joint_index_tensors(self.streams, device)
         return self._idx
 
     def forward(self, keypoints, attention_mask):
-        mods = list(self.streams)
-        xe, ye = coordinate_mapping_grouped([m.coordinate_mapping for m in mods], keypoints,
-                                            self.joint_indices(keypoints.device))
-        out, _ = sca_grouped([m.sca for m in mods], xe, ye, attention_mask)
-        if self.with_residual:
-            out = residual_network_grouped([m.residual for m in mods], out)
-        return out
+        return keypoint_streams_forward(list(self.streams), self.joint_indices(keypoints.device), keypoints,
+                                        attention_mask, self.with_residual)
+
+
+def joint_index_tensors(mods, device):
+    return [torch.tensor(list(m.joint_idx), dtype=torch.int32, device=device) for m in mods]
+
+
+def keypoint_streams_forward(mods, joint_idx, keypoints, attention_mask, with_residual=True):
+    """G KeypointModules in lock-step over one (B, T, K_all, 2) tensor (stream slicing fused)."""
+    xe, ye = coordinate_mapping_grouped([m.coordinate_mapping for m in mods], keypoints, joint_idx)
+    out, _ = sca_grouped([m.sca for m in mods], xe, ye, attention_mask)
+    if with_residual:
+        out = residual_network_grouped([m.residual for m in mods], out)
+    return out

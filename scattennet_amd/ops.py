@@ -643,3 +643,130 @@ class CoordinateMappingOp(Function):
         if pairs:
             reduce_rows(pairs, rows, 1, N, N, 0)
         return (None, dkp) + (None,) * G + tuple(dwx) + tuple(dbx) + tuple(dwy) + tuple(dby)
+
+
+# --------------------------------------------------------------------------- Linear + GELU (+ residual)
+def gelu_bwd(dys, zs):
+    """dz = dy * gelu'(z) for lists of equally sized tensors."""
+    outs = [torch.empty_like(z) for z in zs]
+    for c in range(0, len(zs), L.GELU_MAX_PROBLEMS):
+        gs = range(c, min(len(zs), c + L.GELU_MAX_PROBLEMS))
+        arr = (L.GeluBwdProblem * len(gs))(*[L.GeluBwdProblem(dys[g].data_ptr(), zs[g].data_ptr(),
+                                                              outs[g].data_ptr()) for g in gs])
+        L.check(L.lib().sca_gelu_bwd(len(gs), arr, zs[0].numel(), L.stream_handle()), "sca_gelu_bwd")
+    return outs
+
+
+class LinearGelu(Function):
+    """y = GELU_erf(x W^T + b) (+ r) — the Linear+GELU pairs of model/fusion.py:43-50 and
+    InvertedResidual (:71-77).  The GEMM epilogue applies bias + GELU (and the residual) and
+    keeps the pre-activation for the backward."""
+
+    @staticmethod
+    def forward(ctx, G, has_r, *ts):
+        x = _contig(ts[:G])
+        W, b = ts[G:2 * G], ts[2 * G:3 * G]
+        r = _contig(ts[3 * G:4 * G]) if has_r else [None] * G
+        L.require_device(*x)
+        probs, ys, zs = [], [], []
+        for g in range(G):
+            n_out, n_in = W[g].shape
+            M = x[g].numel() // n_in
+            y = x[g].new_empty(*x[g].shape[:-1], n_out)
+            z = x[g].new_empty(M, n_out)
+            probs.append(_prob([_seg(_flat(x[g]), W[g], n_in, n_in, n_in)], y, M, n_out, n_out, bias=b[g],
+                               resid=r[g], ldr=n_out, epi=L.EPI_GELU, aux_out=z, ldo=n_out))
+            ys.append(y)
+            zs.append(z)
+        gemm(L.GEMM_NT, probs)
+        ctx.G, ctx.has_r, ctx.has_b = G, has_r, [bb is not None for bb in b]
+        ctx.save_for_backward(*x, *W, *zs)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        G = ctx.G
+        sv = ctx.saved_tensors
+        x, W, zs = sv[:G], sv[G:2 * G], sv[2 * G:3 * G]
+        dys = _contig(_zeros_for_none(dys, [x[g].new_empty(*x[g].shape[:-1], W[g].shape[0]) for g in range(G)]))
+        dz = gelu_bwd([_flat(d) for d in dys], zs)
+        probs, dxs = [], []
+        for g in range(G):
+            n_out, n_in = W[g].shape
+            M = x[g].numel() // n_in
+            dx = torch.empty_like(x[g])
+            probs.append(_prob([_seg(dz[g], W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
+            dxs.append(dx)
+        gemm(L.GEMM_NN, probs)
+        wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.has_b[g]) for g in range(G)])
+        return (None, None) + tuple(dxs) + tuple(w for w, _ in wg) + tuple(bb for _, bb in wg) + \
+            (tuple(dys) if ctx.has_r else ())
+
+
+# --------------------------------------------------------------------------- per-clip matmuls
+def _clip_views(t):
+    return [t[i] for i in range(t.shape[0])]
+
+
+class ClipMatmul(Function):
+    """C[b] = A[b] B[b]^T (trans_b) or A[b] B[b], one grouped GEMM problem per clip
+    (CoordinatesFusion's r l^T and attn . body, model/fusion.py:52-55)."""
+
+    @staticmethod
+    def forward(ctx, trans_b, A, Bm):
+        A, Bm = A.contiguous(), Bm.contiguous()
+        L.require_device(A, Bm)
+        nb, m, k = A.shape
+        n = Bm.shape[1] if trans_b else Bm.shape[2]
+        C = A.new_empty(nb, m, n)
+        Av, Bv, Cv = _clip_views(A), _clip_views(Bm), _clip_views(C)
+        if trans_b:
+            probs = [_prob([_seg(Av[i], Bv[i], k, k, k)], Cv[i], m, n, n) for i in range(nb)]
+            gemm(L.GEMM_NT, probs)
+        else:
+            probs = [_prob([_seg(Av[i], Bv[i], k, n, k)], Cv[i], m, n, n) for i in range(nb)]
+            gemm(L.GEMM_NN, probs)
+        ctx.trans_b = trans_b
+        ctx.save_for_backward(A, Bm)
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        A, Bm = ctx.saved_tensors
+        dC = dC.contiguous()
+        nb, m, k = A.shape
+        n = dC.shape[2]
+        dA, dB = torch.empty_like(A), torch.empty_like(Bm)
+        Av, Bv, dCv, dAv, dBv = (_clip_views(t) for t in (A, Bm, dC, dA, dB))
+        if ctx.trans_b:  # C = A B^T:  dA = dC B (NN),  dB = dC^T A (TN)
+            gemm(L.GEMM_NN, [_prob([_seg(dCv[i], Bv[i], n, k, n)], dAv[i], m, k, k) for i in range(nb)])
+            gemm(L.GEMM_TN, [_prob([_seg(dCv[i], Av[i], n, k, m)], dBv[i], n, k, k) for i in range(nb)])
+        else:  # C = A B:  dA = dC B^T (NT),  dB = A^T dC (TN)
+            gemm(L.GEMM_NT, [_prob([_seg(dCv[i], Bv[i], n, n, n)], dAv[i], m, k, k) for i in range(nb)])
+            gemm(L.GEMM_TN, [_prob([_seg(Av[i], dCv[i], k, n, m)], dBv[i], k, n, n) for i in range(nb)])
+        return None, dA, dB
+
+
+class SoftmaxRows(Function):
+    """softmax over the last dim (model/fusion.py:53: no scale, no mask)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        L.require_device(x)
+        N = x.shape[-1]
+        y = torch.empty_like(x)
+        arr = (L.SoftmaxProblem * 1)(L.SoftmaxProblem(x.data_ptr(), None, None, y.data_ptr()))
+        L.check(L.lib().sca_softmax_rows_fwd(1, arr, x.numel() // N, N, L.stream_handle()), "sca_softmax_rows_fwd")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        N = y.shape[-1]
+        dx = torch.empty_like(y)
+        arr = (L.SoftmaxProblem * 1)(L.SoftmaxProblem(None, y.data_ptr(), dy.data_ptr(), dx.data_ptr()))
+        L.check(L.lib().sca_softmax_rows_bwd(1, arr, y.numel() // N, N, L.stream_handle()), "sca_softmax_rows_bwd")
+        return dx

@@ -37,9 +37,37 @@ WORKLOADS = {
     "cfg1": dict(B=2, T=64, K_all=27, groups=[27], d=64, H=4, L=4, residual=False, maxpos=64),
     # BASELINE config 2 — the metric's configuration: four SCA streams of K=79 joints
     "cfg2": dict(B=8, T=256, K_all=79, groups=[6, 21, 21, 31], d=256, H=16, L=4, residual=False, maxpos=256),
-    # BASELINE config 5: long sequence, one 133-joint stream... split COCO-WholeBody
+    # BASELINE config 3: the full encoder with the Phoenix-2014T yaml model section
+    # (configs/phoenix-2014t.yaml:208-277): body/left/right = joints 11-16 / 33-53 / 54-74 of
+    # the (B, T, 542, 2) MediaPipe tensor, residual [256,256,512,512], fusion 512 -> 1024
+    "cfg3": dict(B=8, T=256, K_all=542, groups=[6, 21, 21], d=256, H=16, L=4, residual=True, maxpos=256,
+                 fusion=True, joint_idx=[list(range(11, 17)), list(range(33, 54)), list(range(54, 75))],
+                 residual_blocks=[256, 256, 512, 512], in_fusion=512, out_fusion=1024),
+    # BASELINE config 5: long sequence, 133 joints split COCO-WholeBody style
     "cfg5": dict(B=8, T=1024, K_all=133, groups=[23, 68, 21, 21], d=512, H=16, L=4, residual=False, maxpos=1024),
 }
+
+
+def encoder_cfg(w):
+    """The yaml-style model dict for a fusion workload (SCAEncoder / oracle)."""
+    cfg = model_cfg(w["d"], w["H"], w["L"], maxpos=w["maxpos"], residual_blocks=w["residual_blocks"])
+    cfg.update({"body_idx": w["joint_idx"][0], "left_idx": w["joint_idx"][1], "right_idx": w["joint_idx"][2],
+                "in_fusion_dim": w["in_fusion"], "out_fusion_dim": w["out_fusion"], "num_frame": w["T"]})
+    return cfg
+
+
+def build_encoder(w, device, seed=0, init="reference"):
+    from .encoder import SCAEncoder
+    torch.manual_seed(seed)
+    enc = SCAEncoder(encoder_cfg(w))
+    if init == "reference":
+        init_like_msca(enc)
+    elif init == "random":
+        randomize(enc, seed)
+    # primary throughput runs use p = 0 everywhere (BASELINE.md), including the fusion's
+    # hard-coded 0.2 (model/__init__.py:96)
+    enc.coordinates_fusion.drop_rate = CFG_BASE["dropout"]
+    return enc.to(device)
 
 
 def build_streams(w, device, seed=0, init="reference"):
@@ -94,7 +122,10 @@ def synthetic_batch(w, device, seed=0, ragged=False):
         lens = [T, max(T - 37, 1), T // 2, 1, 0, max(T - 5, 1), T // 4, T][:B]
         for b, n in enumerate(lens):
             mask[b, n:] = 0
-    gout = torch.randn(len(w["groups"]), B, T, w["d"], generator=torch.Generator().manual_seed(1))
+    if w.get("fusion"):
+        gout = torch.randn(1, B, T // 4, w["out_fusion"], generator=torch.Generator().manual_seed(1))
+    else:
+        gout = torch.randn(len(w["groups"]), B, T, w["d"], generator=torch.Generator().manual_seed(1))
     return kp.to(device), mask.to(device), gout.to(device)
 
 
@@ -108,5 +139,16 @@ def flops_per_step(w):
     total = 0.0
     for K in w["groups"]:
         f = L * (24 * N * d * d + 8 * B * T * T * d + 4 * B * d * T * (T + 1) / 2 + 8 * N * d * Fd) + 4 * N * K * d
+        if w.get("residual"):
+            blocks, rows, prev = w.get("residual_blocks", [d, d, 2 * d, 2 * d]), N, None
+            for i, c in enumerate(blocks):
+                cin = blocks[i - 1] if i > 0 else blocks[0]
+                f += 2 * rows * cin * c + 2 * rows * c * c + (2 * rows * cin * c if cin != c else 0)
+                if i % 2 == 0:
+                    rows //= 2
+        total += 3 * f
+    if w.get("fusion"):
+        n4, t4, ci, co = N // 4, T // 4, w["in_fusion"], w["out_fusion"]
+        f = 3 * 2 * n4 * ci * co + 2 * 2 * B * t4 * t4 * co + 2 * n4 * co * co * 2 + 2 * 2 * n4 * co * 3 * co
         total += 3 * f
     return total

@@ -60,6 +60,14 @@ def test_constructor_errors_match_reference():
                                "ff_dim": 64}, "bogus")
 
 
+def test_fusion_state_dict_keys_match_reference():
+    import scattennet_amd as S
+    from tests.golden_util import load
+    fx = load("fusion")
+    m = S.CoordinatesFusion(fx["meta"]["in"], fx["meta"]["out"], 0.2)
+    assert set(m.state_dict().keys()) == set(fx["param"].keys())
+
+
 def test_state_dict_keys_match_reference():
     """Key layout of one KeypointModule equals the reference's (golden fixture keys)."""
     import scattennet_amd as S

@@ -140,3 +140,13 @@ def test_keypoint_module():
     m = _load(S.KeypointModule(list(range(3, 24)), meta["T"], meta["cfg"]), fx, dev)
     i = _inputs(fx, dev, ("keypoints",))
     _check(fx, m, m(i["keypoints"], i["mask"]), i, ("keypoints",))
+
+
+def test_coordinates_fusion():
+    import scattennet_amd as S
+    dev = _dev()
+    fx = load("fusion")
+    m = _load(S.CoordinatesFusion(fx["meta"]["in"], fx["meta"]["out"], 0.2), fx, dev)
+    gi = ("left", "right", "body")
+    i = _inputs(fx, dev, gi)
+    _check(fx, m, m(i["left"], i["right"], i["body"]), i, gi)

@@ -55,3 +55,34 @@ def test_cfg2_four_streams_vs_oracle():
 def test_cfg5_long_sequence_vs_oracle():
     # one stream of the T=1024, d=512 (hd=32) config: the causal y-stream tiles through LDS
     _run("cfg5", W.WORKLOADS["cfg5"], streams_used=1)
+
+
+def test_cfg3_full_encoder_vs_oracle():
+    """BASELINE config 3: yaml model section, 3 streams + residual + fusion, ragged masks."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    w = W.WORKLOADS["cfg3"]
+    enc = W.build_encoder(w, dev, seed=4, init="random").eval()  # parity at eval (dropout off)
+    kp, mask, gout = W.synthetic_batch(w, dev, seed=6, ragged=True)
+    fuse = enc(kp, mask)[0]
+    fuse.backward(gout[0])
+    torch.cuda.synchronize()
+    cfg = W.encoder_cfg(w)
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in enc.state_dict().items()}
+    kpc, mc = kp.cpu(), mask.cpu()
+    streams = {}
+    for name, idx in (("body", cfg["body_idx"]), ("left", cfg["left_idx"]), ("right", cfg["right_idx"])):
+        streams[name] = O.keypoint_module(p, f"{name}_encoder", kpc[:, :, idx, :], mc, cfg)
+    ref = O.coordinates_fusion(p, "coordinates_fusion", streams["left"], streams["right"], streams["body"])
+    assert rel_err(fuse, ref) < PARITY_TOL
+    (ref * gout[0].cpu()).sum().backward()
+    grads = {k: v.grad for k, v in p.items() if v.grad is not None}
+    gscale = max(float(t.abs().max()) for t in grads.values())
+    named = dict(enc.named_parameters())
+    for k, gr in grads.items():
+        assert named[k].grad is not None, k
+        assert close(named[k].grad.cpu(), gr, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), gr))
+    for k, prm in named.items():  # parameters the reference never trains (long shortcuts)
+        if k not in grads:
+            assert prm.grad is None, k
