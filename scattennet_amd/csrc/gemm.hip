@@ -612,12 +612,14 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
 
 int g_tile_override[3] = {0, 0, 0};
 
-// Tile heuristic (measured, tools/gemm_bench.py): at these small per-stream shapes the
-// 64x64 tile wins; see DESIGN.md.
+// Tile heuristic (measured with tools/gemm_bench.py at the workload's shapes, see
+// DESIGN.md): 64x64 / 4 waves for the forward (NT), 128x64 / 8 waves for dX (NN), the
+// single-buffered 64x64 (8 workgroups per CU) for the split-K weight gradients (TN).
 int pick_tile(int layout, long tiles64, int splitk) {
   if (g_tile_override[layout]) return g_tile_override[layout];
-  (void)tiles64;
   (void)splitk;
+  if (layout == SCA_GEMM_NN && tiles64 >= 512) return 7;
+  if (layout == SCA_GEMM_TN) return 5;
   return 1;
 }
 
