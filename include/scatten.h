@@ -102,8 +102,11 @@ int sca_gemm_tile_override(int layout, int tile);
  *   add_mask != NULL                   -> s + add_mask[b, i, j]   (general (B,1,Tq,Tk))
  *   else key_valid != NULL && !valid_j -> finfo.min       (utils.py:3-12)
  *   else                               -> s + (causal && plus_one ? 1 : 0) (utils.py:24-27)
- * Softmax stats are saved per (g,b,h,i) as m (row max) and ll (log of the row sum) so
- * that fully padded rows (all finfo.min) recompute to exactly uniform weights.         */
+ * Softmax stats are saved per (g,b,h,i) in the base-2 domain the kernels compute in
+ * (scores x log2(e)): m (row max) and ll (log2 of the row sum), kept apart so that fully
+ * padded rows (all finfo.min) recompute to exactly uniform weights.  A materialised mask
+ * value so negative that x log2(e) overflows is taken as finfo.min (it only arises from
+ * finfo.min masks, whose sums with a score all round to finfo.min).                    */
 typedef struct {
   const float* q;
   const float* k;

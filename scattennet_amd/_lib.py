@@ -124,6 +124,10 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest
+        # tuning knob: SCA_GEMM_TILES="nt,nn,tn" forces a tile config per layout (0 = heuristic)
+        for layout, t in enumerate(os.environ.get("SCA_GEMM_TILES", "").split(",")):
+            if t.strip():
+                L.sca_gemm_tile_override(layout, int(t))
         _lib = L
     return _lib
 

@@ -7,21 +7,26 @@
 // Layout in HBM: activations stay (B, T, H*hd) row-major exactly as the projections write
 // them (no head transposes: head h is the column slice h*hd .. h*hd+hd-1).
 //
-// Mask encoding (branch-free): every key j of a block gets a pair (mul_j, add_j) in LDS and
-// the masked score is fma(s, mul_j, add_j):
-//   valid key            (1, plus)      plus = 1.0 for the causal mask (utils.py:24-27), else 0
-//   padded key           (0, finfo.min) (utils.py:3-12; s*0 + min == min, as s + min rounds)
-//   key >= Tk            (0, -inf)      (not part of the row at all)
-// With an explicit additive (B,1,Tq,Tk) mask (general path) every key is (1, 0) and the
-// mask value is added.  Causal keys above the diagonal are set to -inf (attention.py:165-169)
-// only in the diagonal blocks (wave-uniform branch).
+// Base-2 domain: a score s becomes t = s*log2(e) + add_j with one fma, where add_j is per
+// key (in LDS):
+//   valid key            plus*log2(e)   plus = 1.0 for the causal mask (utils.py:24-27), else 0
+//   padded key           finfo.min      (utils.py:3-12; s + finfo.min rounds to finfo.min)
+//   key >= Tk            -inf           (not part of the row at all)
+// and p = exp2(t - m) is one raw v_exp_f32.  With an explicit additive (B,1,Tq,Tk) mask
+// (general path) the mask value is added in natural units first.  Causal keys above the
+// diagonal (attention.py:165-169) only exist in the last (diagonal) key block of a query
+// block: that block runs a separately compiled step, every other block is branch-free.
+//
+// LDS images are unpadded and XOR-swizzled so that every ds_read_b128 fragment read is
+// conflict-free in the gfx950 lane groups (row images: swizzle on the float4 slot by the
+// row; transposed images [hd][64]: slot ^ 2*(row & 7)).
 //
 // Forward: one workgroup = (problem g, clip b, head h, 64 queries); 4 waves x 16 queries.
 // K/V stream through LDS in 64-key blocks (register-prefetched one block ahead, one barrier
 // per block).  Scores are computed SWAPPED (S^T = K Q^T) so a lane owns one query column and
 // 4 keys per 16x16 tile: the row max / row sum need two xor-shuffles, and the S^T
 // accumulator registers are already the B operand of O^T += V^T P^T — P never leaves
-// registers.  Online softmax.  Saves m (row max) and ll = log(row sum) per row: a fully
+// registers.  Online softmax.  Saves m (row max) and ll = log2(row sum) per row: a fully
 // padded row (all finfo.min) then recomputes to exactly uniform weights in the backward.
 //
 // Backward: two kernels, no atomics (deterministic):
@@ -29,6 +34,8 @@
 //               dS = P (dP - delta); dQ^T += K^T dS^T.
 //   dkdv kernel (key-block major):   S, dP recomputed with the key on the lane;
 //               dV^T += dO^T P ; dK^T += Q^T dS.
+#include <type_traits>
+
 #include "common.h"
 #include "../../include/scatten.h"
 
@@ -36,7 +43,7 @@ namespace {
 
 constexpr int QB = 64;  // queries per workgroup (16 per wave)
 constexpr int KB = 64;  // keys per LDS block
-constexpr int TP = 4;   // LDS padding (floats)
+constexpr float L2E = SCA_LOG2E;
 
 struct FwdArgs {
   sca_attn_fwd_problem p[SCA_ATTN_MAX_PROBLEMS];
@@ -48,28 +55,30 @@ struct BwdArgs {
   int B, H, Tq, Tk, ldq, ldk, ldv, ldo, causal, plus_one;
 };
 
-// (mul, add) of key j (see header comment).  The validity word is loaded separately
-// (kv_load) so that the compare happens at LDS-commit time: a compare right after the load
-// would make the wave wait for the whole K/V prefetch that was issued with it.
+using DiagStep = std::true_type;
+using FullStep = std::false_type;
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Natural-units masked score -> base-2 domain (general additive-mask path).  Values that
+// overflow to -inf only come from finfo.min masks: they all map to finfo.min.
+__device__ __forceinline__ float to_log2(float t) {
+  const float t2 = t * L2E;
+  return (t2 == -INFINITY && t != -INFINITY) ? SCA_FMIN : t2;
+}
+
+// The validity word is loaded separately (kv_load) so that the compare happens at
+// LDS-commit time: a compare right after the load would make the wave wait for the whole
+// K/V prefetch that was issued with it.
 __device__ __forceinline__ float kv_load(const float* key_valid, int b, int j, int Tk) {
   return key_valid ? key_valid[(long)b * Tk + min(j, Tk - 1)] : 1.f;
 }
 
-__device__ __forceinline__ void key_coef(float kv, bool add_mask, int j, int Tk, float plus, float& mul,
-                                         float& add) {
-  if (j >= Tk) {
-    mul = 0.f;
-    add = -INFINITY;
-  } else if (add_mask) {
-    mul = 1.f;
-    add = 0.f;
-  } else if (kv == 0.f) {
-    mul = 0.f;
-    add = SCA_FMIN;
-  } else {
-    mul = 1.f;
-    add = plus;
-  }
+// per-key additive term in the base-2 domain (see header comment)
+__device__ __forceinline__ float key_add(float kv, bool add_mask, int j, int Tk, float plus2) {
+  if (j >= Tk) return -INFINITY;
+  if (add_mask) return 0.f;
+  return kv == 0.f ? SCA_FMIN : plus2;
 }
 
 // Row block of HD floats per row, 64 rows: each thread owns RV = HD/16 float4 of it.
@@ -78,6 +87,24 @@ struct Blk {
   static constexpr int V4 = HD / 4;          // float4 per row
   static constexpr int RV = 64 * V4 / 256;   // float4 per thread
 };
+
+// float4-slot swizzle of row r in a [64][HD] row image (conflict-free fragment reads)
+template <int HD>
+__device__ __forceinline__ int row_swz(int r) {
+  if constexpr (HD == 16) return (0x78 >> (2 * ((r >> 2) & 3))) & 3;  // [0, 2, 3, 1]
+  else if constexpr (HD == 32) return ((r >> 1) & 1) | (((r >> 2) & 1) << 2);
+  else return (r & 3) | ((r & 4) << 1);
+}
+
+template <int HD>
+__device__ __forceinline__ f32x4 row_frag(const float* img, int row, int slot) {
+  return ld4(img + row * HD + 4 * (slot ^ row_swz<HD>(row)));
+}
+
+// transposed image [HD][64]: 4 consecutive keys/queries at float4 slot `slot` of row d
+__device__ __forceinline__ f32x4 col_frag(const float* img, int d, int slot) {
+  return ld4(img + d * 64 + 4 * (slot ^ (2 * (d & 7))));
+}
 
 template <int HD>
 __device__ __forceinline__ void blk_load(f32x4* r, const float* base, long ld, int r0, int nrows) {
@@ -90,38 +117,52 @@ __device__ __forceinline__ void blk_load(f32x4* r, const float* base, long ld, i
   }
 }
 
-// row image [64][HD+TP] and/or transposed image [HD][64+TP]
 template <int HD>
-__device__ __forceinline__ void blk_store(float* rowimg, float* colimg, const f32x4* r) {
+__device__ __forceinline__ void store_rows(float* img, const f32x4* r) {
+#pragma unroll
+  for (int i = 0; i < Blk<HD>::RV; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int row = e / Blk<HD>::V4, s = e % Blk<HD>::V4;
+    st4(img + row * HD + 4 * (s ^ row_swz<HD>(row)), r[i]);
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ void store_cols(float* img, const f32x4* r) {
 #pragma unroll
   for (int i = 0; i < Blk<HD>::RV; ++i) {
     const int e = threadIdx.x + 256 * i;
     const int row = e / Blk<HD>::V4, c = (e % Blk<HD>::V4) * 4;
-    if (rowimg) st4(rowimg + row * (HD + TP) + c, r[i]);
-    if (colimg) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) colimg[(c + j) * (64 + TP) + row] = r[i][j];
+    for (int j = 0; j < 4; ++j) {
+      const int d = c + j;
+      img[d * 64 + 4 * ((row >> 2) ^ (2 * (d & 7))) + (row & 3)] = r[i][j];
     }
   }
 }
 
 // ------------------------------------------------------------------------------ forward
-template <int HD, bool ADDMASK>
+template <int HD, bool ADDMASK, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
   constexpr int NS = HD / 4;   // MFMA k-steps over the head dim
   constexpr int ND = HD / 16;  // 16-wide output d-blocks
   constexpr int RV = Blk<HD>::RV;
-  __shared__ __attribute__((aligned(16))) float Ks[2][KB * (HD + TP)];
-  __shared__ __attribute__((aligned(16))) float Vt[2][HD * (KB + TP)];
-  __shared__ __attribute__((aligned(16))) float Km[2][KB], Ka[2][KB];
+  __shared__ __attribute__((aligned(16))) float Ks[2][KB * HD];
+  __shared__ __attribute__((aligned(16))) float Vt[2][HD * KB];
+  __shared__ __attribute__((aligned(16))) float Ka[2][KB];
 
   const sca_attn_fwd_problem& P = a.p[blockIdx.z];
   const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
-  const int q0 = blockIdx.x * QB;
+  const int nqb = (a.Tq + QB - 1) / QB;  // causal: block x is paired with block nqb-1-x
+  const int jobs = (CAUSAL && nqb - 1 - (int)blockIdx.x != (int)blockIdx.x) ? 2 : 1;
+#pragma unroll 1
+  for (int job = 0; job < jobs; ++job) {
+  const int xb = job ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int q0 = xb * QB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = lane & 15, grp = lane >> 4;
   const int qrow = q0 + 16 * w + qi;
-  const float plus = (a.causal && a.plus_one) ? 1.0f : 0.0f;
+  const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
 
   // Q fragment: lane holds Q[qrow][NS*grp + s], s < NS (B operand of S^T = K Q^T)
   float qreg[NS];
@@ -141,9 +182,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
   for (int d = 0; d < ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
-  const int kend = a.causal ? min(a.Tk, q0 + QB) : a.Tk;
-  const int nblk = (kend + KB - 1) / KB;
-  const int wave_qmin = q0 + 16 * w, wave_qmax = wave_qmin + 15;
+  // causal: Tq == Tk and QB == KB, so the last key block is the diagonal one
+  const int nblk = CAUSAL ? xb + 1 : (a.Tk + KB - 1) / KB;
   const float* kbase = P.k + (long)b * a.Tk * a.ldk + h * HD;
   const float* vbase = P.v + (long)b * a.Tk * a.ldv + h * HD;
 
@@ -157,51 +197,42 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
     kbn = kb;
   };
   auto commit = [&](int buf) {
-    blk_store<HD>(Ks[buf], nullptr, rk);
-    blk_store<HD>(nullptr, Vt[buf], rv);
-    if (threadIdx.x < KB) {
-      float cm, ca;
-      key_coef(kvraw, ADDMASK, kbn + threadIdx.x, a.Tk, plus, cm, ca);
-      Km[buf][threadIdx.x] = cm;
-      Ka[buf][threadIdx.x] = ca;
-    }
+    store_rows<HD>(Ks[buf], rk);
+    store_cols<HD>(Vt[buf], rv);
+    if (threadIdx.x < KB) Ka[buf][threadIdx.x] = key_add(kvraw, ADDMASK, kbn + threadIdx.x, a.Tk, plus2);
   };
   prefetch(0);
   commit(0);
   __syncthreads();
 
-  for (int blk = 0; blk < nblk; ++blk) {
+  auto step = [&](auto diag_c, int blk) {
+    constexpr bool DIAG = decltype(diag_c)::value;
     const int kb = blk * KB, buf = blk & 1;
-
+    const bool more = blk + 1 < nblk;
     float sv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const bool live = !a.causal || (kb + 16 * t <= wave_qmax);
-      if (!live) {
+      if (DIAG && t > w) {  // wave-uniform: the whole tile is above the diagonal
 #pragma unroll
         for (int r = 0; r < 4; ++r) sv[t][r] = -INFINITY;
         continue;
       }
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* kr = Ks[buf] + (16 * t + qi) * (HD + TP) + NS * grp;
 #pragma unroll
       for (int s = 0; s < NS; s += 4) {
-        const f32x4 kv = ld4(kr + s);
+        const f32x4 kv = row_frag<HD>(Ks[buf], 16 * t + qi, (NS * grp + s) >> 2);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc = mfma16(kv[j], qreg[s + j], acc);
       }
       const int kl = 16 * t + 4 * grp;
-      const f32x4 mm = ld4(&Km[buf][kl]), aa = ld4(&Ka[buf][kl]);
+      const f32x4 ad = ld4(&Ka[buf][kl]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = fmaf(acc[r], mm[r], aa[r]);
-        if (ADDMASK && kb + kl + r < a.Tk) s += amrow[kb + kl + r];
-        sv[t][r] = s;
-      }
-      if (a.causal && kb + 16 * t + 15 > wave_qmin) {  // diagonal sub-tile
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (kb + kl + r > qrow) sv[t][r] = -INFINITY;
+        float t2;
+        if (ADDMASK) t2 = to_log2(acc[r] + (kb + kl + r < a.Tk ? amrow[kb + kl + r] : 0.f) + ad[r]);
+        else t2 = fmaf(acc[r], L2E, ad[r]);
+        if (DIAG && t == w && 4 * grp + r > qi) t2 = -INFINITY;
+        sv[t][r] = t2;
       }
     }
     // online softmax (row = this lane's query; 16 values here, 64 across the 4 lanes)
@@ -213,35 +244,38 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
     mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float m_new = fmaxf(m_run, mloc);  // finite after block 0 (key 0 is always in the row)
-    const float alpha = exp2f((m_run - m_new) * SCA_LOG2E);
+    const float alpha = fast_exp2(m_run - m_new);
     m_run = m_new;
     float psum = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f((sv[t][r] - m_new) * SCA_LOG2E);
+        const float p = fast_exp2(sv[t][r] - m_new);
         sv[t][r] = p;
         psum += p;
       }
     l_run = l_run * alpha + psum;
 #pragma unroll
     for (int d = 0; d < ND; ++d) o[d] *= alpha;
-    if (blk + 1 < nblk) prefetch(kb + KB);  // in flight during the P.V MFMAs and the barrier
+    if (more) prefetch(kb + KB);  // in flight during the P.V MFMAs and the barrier
     // O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (a.causal && kb + 16 * t > wave_qmax) continue;
+      if (DIAG && t > w) continue;
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        const f32x4 vv = ld4(Vt[buf] + (16 * d + qi) * (KB + TP) + 16 * t + 4 * grp);
+        const f32x4 vv = col_frag(Vt[buf], 16 * d + qi, 4 * t + grp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[d] = mfma16(vv[r], sv[t][r], o[d]);
       }
     }
-    if (blk + 1 < nblk) commit(buf ^ 1);
+    if (more) commit(buf ^ 1);
     __syncthreads();
-  }
+  };
+  for (int blk = 0; blk + (CAUSAL ? 1 : 0) < nblk; ++blk) step(FullStep{}, blk);
+  if (CAUSAL) step(DiagStep{}, nblk - 1);
+
   float l_tot = l_run + __shfl_xor(l_run, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
   if (qrow < a.Tq) {
@@ -252,31 +286,37 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
     if (grp == 0) {
       const long si = ((long)b * a.H + h) * a.Tq + qrow;
       P.stat_m[si] = m_run;
-      P.stat_ll[si] = logf(l_tot);
+      P.stat_ll[si] = log2f(l_tot);
     }
   }
+  }  // job
 }
 
 // ------------------------------------------------------------------------------ backward: dQ
-template <int HD, bool ADDMASK>
+template <int HD, bool ADDMASK, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   constexpr int NS = HD / 4;
   constexpr int ND = HD / 16;
   constexpr int RV = Blk<HD>::RV;
-  __shared__ __attribute__((aligned(16))) float Ks[2][KB * (HD + TP)];
-  __shared__ __attribute__((aligned(16))) float Vs[2][KB * (HD + TP)];
-  __shared__ __attribute__((aligned(16))) float Kt[2][HD * (KB + TP)];
-  __shared__ __attribute__((aligned(16))) float Km[2][KB], Ka[2][KB];
+  __shared__ __attribute__((aligned(16))) float Ks[2][KB * HD];
+  __shared__ __attribute__((aligned(16))) float Vs[2][KB * HD];
+  __shared__ __attribute__((aligned(16))) float Kt[2][HD * KB];
+  __shared__ __attribute__((aligned(16))) float Ka[2][KB];
 
   const sca_attn_bwd_problem& P = a.p[blockIdx.z];
   const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
-  const int q0 = blockIdx.x * QB;
+  const int nqb = (a.Tq + QB - 1) / QB;  // causal: block x is paired with block nqb-1-x
+  const int jobs = (CAUSAL && nqb - 1 - (int)blockIdx.x != (int)blockIdx.x) ? 2 : 1;
+#pragma unroll 1
+  for (int job = 0; job < jobs; ++job) {
+  const int xb = job ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int q0 = xb * QB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = lane & 15, grp = lane >> 4;
   const int qrow = q0 + 16 * w + qi;
   const bool qok = qrow < a.Tq;
   const int qc = min(qrow, a.Tq - 1);
-  const float plus = (a.causal && a.plus_one) ? 1.0f : 0.0f;
+  const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
 
   float qreg[NS], doreg[NS];
   float dpart = 0.f;
@@ -308,9 +348,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
 #pragma unroll
   for (int d = 0; d < ND; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int kend = a.causal ? min(a.Tk, q0 + QB) : a.Tk;
-  const int nblk = (kend + KB - 1) / KB;
-  const int wave_qmin = q0 + 16 * w, wave_qmax = wave_qmin + 15;
+  const int nblk = CAUSAL ? xb + 1 : (a.Tk + KB - 1) / KB;
   const float* kbase = P.k + (long)b * a.Tk * a.ldk + h * HD;
   const float* vbase = P.v + (long)b * a.Tk * a.ldv + h * HD;
   f32x4 rk[RV], rv[RV];
@@ -323,31 +361,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
     kbn = kb;
   };
   auto commit = [&](int buf) {
-    blk_store<HD>(Ks[buf], Kt[buf], rk);
-    blk_store<HD>(Vs[buf], nullptr, rv);
-    if (threadIdx.x < KB) {
-      float cm, ca;
-      key_coef(kvraw, ADDMASK, kbn + threadIdx.x, a.Tk, plus, cm, ca);
-      Km[buf][threadIdx.x] = cm;
-      Ka[buf][threadIdx.x] = ca;
-    }
+    store_rows<HD>(Ks[buf], rk);
+    store_cols<HD>(Kt[buf], rk);
+    store_rows<HD>(Vs[buf], rv);
+    if (threadIdx.x < KB) Ka[buf][threadIdx.x] = key_add(kvraw, ADDMASK, kbn + threadIdx.x, a.Tk, plus2);
   };
   prefetch(0);
   commit(0);
   __syncthreads();
 
-  for (int blk = 0; blk < nblk; ++blk) {
+  auto step = [&](auto diag_c, int blk) {
+    constexpr bool DIAG = decltype(diag_c)::value;
     const int kb = blk * KB, buf = blk & 1;
-    if (blk + 1 < nblk) prefetch(kb + KB);
+    const bool more = blk + 1 < nblk;
+    if (more) prefetch(kb + KB);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (a.causal && kb + 16 * t > wave_qmax) continue;
+      if (DIAG && t > w) continue;
       f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = s_acc;
-      const float* kr = Ks[buf] + (16 * t + qi) * (HD + TP) + NS * grp;
-      const float* vr = Vs[buf] + (16 * t + qi) * (HD + TP) + NS * grp;
 #pragma unroll
       for (int s = 0; s < NS; s += 4) {
-        const f32x4 kv = ld4(kr + s), vv = ld4(vr + s);
+        const f32x4 kv = row_frag<HD>(Ks[buf], 16 * t + qi, (NS * grp + s) >> 2);
+        const f32x4 vv = row_frag<HD>(Vs[buf], 16 * t + qi, (NS * grp + s) >> 2);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           s_acc = mfma16(kv[j], qreg[s + j], s_acc);
@@ -355,54 +390,62 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
         }
       }
       const int kl = 16 * t + 4 * grp;
-      const f32x4 mm = ld4(&Km[buf][kl]), aa = ld4(&Ka[buf][kl]);
-      const bool diag = a.causal && kb + 16 * t + 15 > wave_qmin;
+      const f32x4 ad = ld4(&Ka[buf][kl]);
       float ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = fmaf(s_acc[r], mm[r], aa[r]);
-        if (ADDMASK && kb + kl + r < a.Tk) s += amrow[kb + kl + r];
-        if (diag && kb + kl + r > qrow) s = -INFINITY;
-        const float p = exp2f(((s - mrow) - llrow) * SCA_LOG2E);
+        float t2;
+        if (ADDMASK) t2 = to_log2(s_acc[r] + (kb + kl + r < a.Tk ? amrow[kb + kl + r] : 0.f) + ad[r]);
+        else t2 = fmaf(s_acc[r], L2E, ad[r]);
+        if (DIAG && t == w && 4 * grp + r > qi) t2 = -INFINITY;
+        const float p = fast_exp2((t2 - mrow) - llrow);
         ds[r] = p * (dp_acc[r] - delta);
       }
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        const f32x4 kt = ld4(Kt[buf] + (16 * d + qi) * (KB + TP) + 16 * t + 4 * grp);
+        const f32x4 kt = col_frag(Kt[buf], 16 * d + qi, 4 * t + grp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) dq[d] = mfma16(kt[r], ds[r], dq[d]);
       }
     }
-    if (blk + 1 < nblk) commit(buf ^ 1);
+    if (more) commit(buf ^ 1);
     __syncthreads();
-  }
+  };
+  for (int blk = 0; blk + (CAUSAL ? 1 : 0) < nblk; ++blk) step(FullStep{}, blk);
+  if (CAUSAL) step(DiagStep{}, nblk - 1);
+
   if (qok) {
     float* dqp = P.dq + ((long)b * a.Tq + qrow) * a.ldq + h * HD + 4 * grp;
 #pragma unroll
     for (int d = 0; d < ND; ++d) st4(dqp + 16 * d, dq[d] * P.dq_scale);
   }
+  }  // job
 }
 
 // ------------------------------------------------------------------------------ backward: dK, dV
-template <int HD, bool ADDMASK>
+template <int HD, bool ADDMASK, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
   constexpr int NS = HD / 4;
   constexpr int ND = HD / 16;
   constexpr int RV = Blk<HD>::RV;
-  __shared__ __attribute__((aligned(16))) float Qs[2][QB * (HD + TP)];
-  __shared__ __attribute__((aligned(16))) float Ds[2][QB * (HD + TP)];
-  __shared__ __attribute__((aligned(16))) float Qt[2][HD * (QB + TP)];
-  __shared__ __attribute__((aligned(16))) float Dt[2][HD * (QB + TP)];
+  __shared__ __attribute__((aligned(16))) float Qs[2][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Ds[2][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Qt[2][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Dt[2][HD * QB];
   __shared__ __attribute__((aligned(16))) float Sm[2][QB], Sl[2][QB], Sd[2][QB];
 
   const sca_attn_bwd_problem& P = a.p[blockIdx.z];
   const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
-  const int k0 = blockIdx.x * KB;
+  const int nkb = (a.Tk + KB - 1) / KB;  // causal: key block x is paired with block nkb-1-x
+  const int jobs = (CAUSAL && nkb - 1 - (int)blockIdx.x != (int)blockIdx.x) ? 2 : 1;
+#pragma unroll 1
+  for (int job = 0; job < jobs; ++job) {
+  const int k0 = (job ? nkb - 1 - (int)blockIdx.x : (int)blockIdx.x) * KB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kj = lane & 15, grp = lane >> 4;
   const int krow = k0 + 16 * w + kj;
   const bool kok = krow < a.Tk;
-  const float plus = (a.causal && a.plus_one) ? 1.0f : 0.0f;
+  const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
 
   float kreg[NS], vreg[NS];
   {
@@ -419,16 +462,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
       }
     }
   }
-  float kmul, kadd;
-  key_coef(kv_load(P.key_valid, b, krow, a.Tk), ADDMASK, krow, a.Tk, plus, kmul, kadd);
+  const float kadd = key_add(kv_load(P.key_valid, b, krow, a.Tk), ADDMASK, krow, a.Tk, plus2);
 
   f32x4 dk[ND], dv[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) dk[d] = dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int qbeg = a.causal ? (k0 / QB) * QB : 0;
+  // causal: the first query block is the diagonal one (QB == KB, Tq == Tk)
+  const int qbeg = CAUSAL ? k0 : 0;
   const int nblk = (a.Tq - qbeg + QB - 1) / QB;
-  const int wave_kmin = k0 + 16 * w, wave_kmax = wave_kmin + 15;
   const float* qbase = P.q + (long)b * a.Tq * a.ldq + h * HD;
   const float* dbase = P.dout + (long)b * a.Tq * a.ldo + h * HD;
   f32x4 rq[RV], rd[RV];
@@ -442,11 +484,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
       cm = P.stat_m[si];
       cl = P.stat_ll[si];
       cd = P.delta[si];
+      if (q >= a.Tq) cm = INFINITY;  // rows past the end: p = exp2(-inf) = 0
     }
   };
   auto commit = [&](int buf) {
-    blk_store<HD>(Qs[buf], Qt[buf], rq);
-    blk_store<HD>(Ds[buf], Dt[buf], rd);
+    store_rows<HD>(Qs[buf], rq);
+    store_cols<HD>(Qt[buf], rq);
+    store_rows<HD>(Ds[buf], rd);
+    store_cols<HD>(Dt[buf], rd);
     if (threadIdx.x < QB) {
       Sm[buf][threadIdx.x] = cm;
       Sl[buf][threadIdx.x] = cl;
@@ -457,18 +502,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
   commit(0);
   __syncthreads();
 
-  for (int blk = 0; blk < nblk; ++blk) {
+  auto step = [&](auto diag_c, int blk) {
+    constexpr bool DIAG = decltype(diag_c)::value;
     const int qb = qbeg + blk * QB, buf = blk & 1;
-    if (blk + 1 < nblk) prefetch(qb + QB);
+    const bool more = blk + 1 < nblk;
+    if (more) prefetch(qb + QB);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (a.causal && qb + 16 * t + 15 < wave_kmin) continue;  // all queries before all keys
+      if (DIAG && t < w) continue;  // wave-uniform: every query of the tile precedes every key
       f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = s_acc;
-      const float* qr = Qs[buf] + (16 * t + kj) * (HD + TP) + NS * grp;
-      const float* dr = Ds[buf] + (16 * t + kj) * (HD + TP) + NS * grp;
 #pragma unroll
       for (int s = 0; s < NS; s += 4) {
-        const f32x4 qv = ld4(qr + s), dv4 = ld4(dr + s);
+        const f32x4 qv = row_frag<HD>(Qs[buf], 16 * t + kj, (NS * grp + s) >> 2);
+        const f32x4 dv4 = row_frag<HD>(Ds[buf], 16 * t + kj, (NS * grp + s) >> 2);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           s_acc = mfma16(qv[j], kreg[s + j], s_acc);
@@ -478,22 +524,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
       // lane holds S[q = qb + 16t + 4grp + r][krow]
       const int ql = 16 * t + 4 * grp;
       const f32x4 sm = ld4(&Sm[buf][ql]), sl = ld4(&Sl[buf][ql]), sd = ld4(&Sd[buf][ql]);
-      const bool diag = a.causal && qb + 16 * t < wave_kmax;
       float p[4], ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int q = qb + ql + r;
-        float s = fmaf(s_acc[r], kmul, kadd);
-        if (ADDMASK && q < a.Tq && krow < a.Tk) s += P.add_mask[((long)b * a.Tq + q) * a.Tk + krow];
-        if (diag && krow > q) s = -INFINITY;
-        if (q >= a.Tq) s = -INFINITY;
-        p[r] = exp2f(((s - sm[r]) - sl[r]) * SCA_LOG2E);
+        float t2;
+        if (ADDMASK) {
+          const int q = min(qb + ql + r, a.Tq - 1);
+          t2 = to_log2(s_acc[r] + (kok ? P.add_mask[((long)b * a.Tq + q) * a.Tk + krow] : 0.f) + kadd);
+        } else {
+          t2 = fmaf(s_acc[r], L2E, kadd);
+        }
+        if (DIAG && t == w && kj > 4 * grp + r) t2 = -INFINITY;
+        p[r] = fast_exp2((t2 - sm[r]) - sl[r]);
         ds[r] = p[r] * (dp_acc[r] - sd[r]);
       }
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        const f32x4 dt = ld4(Dt[buf] + (16 * d + kj) * (QB + TP) + 16 * t + 4 * grp);
-        const f32x4 qt = ld4(Qt[buf] + (16 * d + kj) * (QB + TP) + 16 * t + 4 * grp);
+        const f32x4 dt = col_frag(Dt[buf], 16 * d + kj, 4 * t + grp);
+        const f32x4 qt = col_frag(Qt[buf], 16 * d + kj, 4 * t + grp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           dv[d] = mfma16(dt[r], p[r], dv[d]);
@@ -501,9 +549,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
         }
       }
     }
-    if (blk + 1 < nblk) commit(buf ^ 1);
+    if (more) commit(buf ^ 1);
     __syncthreads();
-  }
+  };
+  int blk = 0;
+  if (CAUSAL) step(DiagStep{}, blk++);
+  for (; blk < nblk; ++blk) step(FullStep{}, blk);
+
   if (kok) {
     float* dkp = P.dk + ((long)b * a.Tk + krow) * a.ldk + h * HD + 4 * grp;
     float* dvp = P.dv + ((long)b * a.Tk + krow) * a.ldv + h * HD + 4 * grp;
@@ -513,6 +565,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
       st4(dvp + 16 * d, dv[d] * P.dv_scale);
     }
   }
+  }  // job
 }
 
 template <typename Args>
@@ -527,13 +580,19 @@ int check_common(const Args& a, int hd, int nprob) {
 
 template <int HD, bool AM>
 void launch_fwd(const FwdArgs& a, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((attn_fwd_kernel<HD, AM>), grid, dim3(256), 0, st, a);
+  if (a.causal) hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, false>), grid, dim3(256), 0, st, a);
 }
 
 template <int HD, bool AM>
 void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st) {
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM>), gq, dim3(256), 0, st, a);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM>), gk, dim3(256), 0, st, a);
+  if (a.causal) {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, true>), gq, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, true>), gk, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, false>), gq, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, false>), gk, dim3(256), 0, st, a);
+  }
 }
 
 }  // namespace
@@ -564,7 +623,8 @@ extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B,
     }
     am = probs[i].add_mask != nullptr;
   }
-  dim3 grid((Tq + QB - 1) / QB, B * H, nprob);
+  const int nqb = (Tq + QB - 1) / QB;  // causal: two paired query blocks per workgroup
+  dim3 grid(causal ? (nqb + 1) / 2 : nqb, B * H, nprob);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hd == 16) am ? launch_fwd<16, true>(a, grid, st) : launch_fwd<16, false>(a, grid, st);
   else if (hd == 32) am ? launch_fwd<32, true>(a, grid, st) : launch_fwd<32, false>(a, grid, st);
@@ -599,7 +659,8 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
     a.p[i] = p;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  dim3 gq((Tq + QB - 1) / QB, B * H, nprob), gk((Tk + KB - 1) / KB, B * H, nprob);
+  const int nqb = (Tq + QB - 1) / QB, nkb = (Tk + KB - 1) / KB;  // causal: paired blocks
+  dim3 gq(causal ? (nqb + 1) / 2 : nqb, B * H, nprob), gk(causal ? (nkb + 1) / 2 : nkb, B * H, nprob);
   if (hd == 16) am ? launch_bwd<16, true>(a, gq, gk, st) : launch_bwd<16, false>(a, gq, gk, st);
   else if (hd == 32) am ? launch_bwd<32, true>(a, gq, gk, st) : launch_bwd<32, false>(a, gq, gk, st);
   else am ? launch_bwd<64, true>(a, gq, gk, st) : launch_bwd<64, false>(a, gq, gk, st);
