@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one captured hipGraph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dropout", type=float, default=0.0,
+                    help="train-mode dropout p for every block (the yaml's 0.2 = the secondary run)")
     return ap.parse_args()
 
 
@@ -59,6 +61,14 @@ def main():
 
     fusion = bool(w.get("fusion"))
     model = W.build_encoder(w, dev, seed=0) if fusion else W.build_streams(w, dev, seed=0, init="reference")
+    if args.dropout > 0:  # secondary run: the yaml's dropout (keypoint_module / layers / fusion)
+        from scattennet_amd import (CoordinateAttention, CoordinatesFusion, CoordinatesMerge, FeedForward,
+                                    SeparativeCoordinateAttention)
+        for m in model.modules():
+            if isinstance(m, (CoordinateAttention, CoordinatesMerge, FeedForward, SeparativeCoordinateAttention)):
+                m.dropout = args.dropout
+            elif isinstance(m, CoordinatesFusion):
+                m.drop_rate = args.dropout
     if world > 1:  # identical initial weights on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
@@ -68,6 +78,8 @@ def main():
     params = [p for p in model.parameters()]
 
     def fwd_bwd():
+        if args.dropout > 0:
+            ops.advance_dropout()  # device-side step counter: fresh masks on every graph replay
         outs = model(kp, mask)
         outs = outs[:1] if fusion else outs  # config 3: the loss seed sits on the fusion output
         torch.autograd.backward(outs, grads_out)
@@ -145,7 +157,7 @@ def main():
                 "step_frac": round(step_flops / (ms / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not fusion:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not fusion and args.dropout == 0:
         cpu = cpu_baseline(w, model, args.cpu_seconds)
 
     if rank == 0:
@@ -156,7 +168,7 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (U[0,1) keypoints, MSCA_Net init)",
             "config": {"workload": f"{args.workload}: " + describe(w), "clips_per_gpu": w["B"], "frames": w["T"],
                        "joints": w["K_all"], "streams": w["groups"], "d_model": w["d"], "heads": w["H"],
-                       "layers": w["L"], "dropout": 0.0, "hipgraph": graph is not None,
+                       "layers": w["L"], "dropout": args.dropout, "hipgraph": graph is not None,
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,

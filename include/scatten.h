@@ -26,6 +26,9 @@
  *   sca_softmax_rows_*     CoordinatesFusion softmax (fusion.py:52-53)
  *   sca_gelu_bwd           GELU backward where no GEMM epilogue can absorb it
  *                          (fusion.py:43-50,74-77)
+ *   sca_dropout            F.dropout in training mode (keypoint_module.py:64,100,164-165,
+ *                          layers.py:105,107, fusion.py:48,54) with a counter-based mask;
+ *                          also fused into the GEMM and LayerNorm epilogues
  */
 #ifndef SCATTEN_H
 #define SCATTEN_H
@@ -49,11 +52,16 @@ extern "C" {
 /* Epilogue flags (applied in this order):
  *   v = acc ; v += bias[n] ; v *= post_scale ;
  *   GELU : aux_out[m,n] = v ; v = gelu_erf(v)
+ *   DROPOUT: v *= keep(drop_seed, m*N + n) / (1 - drop_p)   (see sca_dropout)
  *   DGELU: v *= gelu_erf'(aux[m,n])
- *   v += resid[m,n] (if resid) ; ACCUM: v += C[m,n] ; C[m,n] = v                     */
+ *   v += resid[m,n] (if resid) ; ACCUM: v += C[m,n] ; C[m,n] = v
+ * so the post-LN blocks' y = x + dropout(Linear(h)) (keypoint_module.py:64,100 and
+ * layers.py:105,107) is one epilogue, and the backward of dropout(GELU(z)) is DROPOUT|DGELU
+ * with the forward's seed.                                                             */
 #define SCA_EPI_GELU 1
 #define SCA_EPI_DGELU 2
 #define SCA_EPI_ACCUM 4
+#define SCA_EPI_DROPOUT 8
 
 typedef struct {
   const float* A;
@@ -82,6 +90,8 @@ typedef struct {
    * gradient colsum(dY), fused into the weight-gradient GEMM), or NULL */
   float* bias_grad;
   float bias_grad_scale;
+  unsigned long long drop_seed; /* DROPOUT: per-call seed (one mask per seed) */
+  float drop_p;                 /* DROPOUT: drop probability in [0, 1) */
 } sca_gemm_problem;
 
 /* Grouped GEMM over `nprob` independent problems (e.g. q/k/v x streams).
@@ -147,6 +157,9 @@ int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B, int H, int
  * r row index = (row % r_mod) + r_off  (r_mod = rows for an ordinary residual; r_mod = T,
  * r_off = 2 for the LearningPositionEmbedding table); post (or NULL) is row-aligned with x;
  * act: 0 = identity, 1 = ReLU (ResidualBlock, model/residual.py:31-38).
+ * drop_p > 0 (act must be identity): y = dropout(y) with the sca_dropout mask of
+ * drop_seed — the embedding dropout after first_*_norm (keypoint_module.py:164-165); the
+ * backward applies the same mask to dy (sca_dropout) before sca_layernorm_bwd.
  * Saves mean/rstd per row.                                                              */
 #define SCA_ACT_NONE 0
 #define SCA_ACT_RELU 1
@@ -160,6 +173,8 @@ typedef struct {
   float* mean;
   float* rstd;
   int act;
+  unsigned long long drop_seed;
+  float drop_p;
 } sca_ln_fwd_problem;
 
 typedef struct {
@@ -220,6 +235,31 @@ typedef struct {
 } sca_gelu_bwd_problem;
 #define SCA_GELU_MAX_PROBLEMS 8
 int sca_gelu_bwd(int nprob, const sca_gelu_bwd_problem* probs, long n, void* stream);
+
+/* Dropout (F.dropout, training mode) over contiguous (rows, cols) tensors:
+ *   y[e] = x[e] * keep(seed, e) / (1 - p),  e = row * cols + col
+ * keep() is a counter-based hash RNG (no state, no sequence): with
+ *   mix(x) = lowbias32 (x^=x>>16; x*=0x7feb352d; x^=x>>15; x*=0x846ca68b; x^=x>>16),
+ *   key = mix(lo32(seed) ^ mix(hi32(seed) + 0x9e3779b9)),
+ *   keep = mix(mix(e ^ key) + key) >= (uint32)(p * 2^32 in fp32)
+ * so forward, backward and the CPU oracle regenerate the same mask from the seed alone
+ * (masks differ from torch's Philox stream; the drop rate is the same).  The same mask
+ * is applied by the GEMM DROPOUT epilogue and the LayerNorm forward.  In-place allowed.
+ * Used for: the backward of every dropout site, and the fusion's attention-weight and
+ * output dropout (model/fusion.py:48,54).                                               */
+typedef struct {
+  const float* x;
+  float* y;
+  unsigned long long seed;
+} sca_dropout_problem;
+#define SCA_DROPOUT_MAX_PROBLEMS 12
+int sca_dropout(int nprob, const sca_dropout_problem* probs, long rows, int cols, float p, void* stream);
+
+/* Registers a device-resident step counter (or NULL) read by every dropout mask at run
+ * time: effective seed = seed + counter * 0x9E3779B97F4A7C15.  A hipGraph that captures
+ * the counter's increment then draws fresh masks on every replay although the seeds in
+ * its kernel arguments are frozen.  Process-global; applies to launches issued after. */
+int sca_dropout_offset(const unsigned long long* counter);
 
 /* out[i, j] (+)= scale * sum_{s < S} in[s * stride_s + i * stride_i + j],  i < I, j < N.
  * Column sums (bias gradients), slab reductions, position-table gradients.            */

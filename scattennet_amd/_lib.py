@@ -13,9 +13,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libscatten_hip.so")
 
 c_int, c_float, c_long, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_long, ctypes.c_void_p
+c_u64 = ctypes.c_uint64
 
 GEMM_NT, GEMM_NN, GEMM_TN = 0, 1, 2
-EPI_GELU, EPI_DGELU, EPI_ACCUM = 1, 2, 4
+EPI_GELU, EPI_DGELU, EPI_ACCUM, EPI_DROPOUT = 1, 2, 4, 8
 GEMM_MAX_PROBLEMS = 12
 ATTN_MAX_PROBLEMS = 8
 LN_MAX_PROBLEMS = 8
@@ -24,6 +25,7 @@ MAP_MAX_PROBLEMS = 8
 POOL_MAX_PROBLEMS = 8
 SOFTMAX_MAX_PROBLEMS = 8
 GELU_MAX_PROBLEMS = 8
+DROPOUT_MAX_PROBLEMS = 12
 ACT_NONE, ACT_RELU = 0, 1
 
 
@@ -35,7 +37,7 @@ class GemmProblem(ctypes.Structure):
     _fields_ = [("seg", GemmSeg * 3), ("nseg", c_int), ("M", c_int), ("N", c_int), ("C", c_void_p), ("ldc", c_int),
                 ("epi", c_int), ("bias", c_void_p), ("post_scale", c_float), ("resid", c_void_p), ("ldr", c_int),
                 ("aux", c_void_p), ("ldx", c_int), ("aux_out", c_void_p), ("ldo", c_int), ("bias_grad", c_void_p),
-                ("bias_grad_scale", c_float)]
+                ("bias_grad_scale", c_float), ("drop_seed", c_u64), ("drop_p", c_float)]
 
 
 class AttnFwdProblem(ctypes.Structure):
@@ -52,7 +54,8 @@ class AttnBwdProblem(ctypes.Structure):
 
 class LnFwdProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("r", c_void_p), ("gamma", c_void_p), ("beta", c_void_p), ("post", c_void_p),
-                ("y", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("act", c_int)]
+                ("y", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("act", c_int), ("drop_seed", c_u64),
+                ("drop_p", c_float)]
 
 
 class LnBwdProblem(ctypes.Structure):
@@ -71,6 +74,10 @@ class SoftmaxProblem(ctypes.Structure):
 
 class GeluBwdProblem(ctypes.Structure):
     _fields_ = [("dy", c_void_p), ("z", c_void_p), ("dz", c_void_p)]
+
+
+class DropoutProblem(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("seed", c_u64)]
 
 
 class ReduceProblem(ctypes.Structure):
@@ -101,6 +108,8 @@ EXPORTS = {
     "sca_softmax_rows_fwd": ([c_int, c_void_p, c_int, c_int, c_void_p], c_int),
     "sca_softmax_rows_bwd": ([c_int, c_void_p, c_int, c_int, c_void_p], c_int),
     "sca_gelu_bwd": ([c_int, c_void_p, c_long, c_void_p], c_int),
+    "sca_dropout": ([c_int, c_void_p, c_long, c_int, c_float, c_void_p], c_int),
+    "sca_dropout_offset": ([c_void_p], c_int),
     "sca_reduce_rows": ([c_int, c_void_p, c_int, c_int, c_int, c_long, c_long, c_int, c_void_p], c_int),
     "sca_coord_map_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_coord_map_bwd_chunks": ([c_int], c_int),

@@ -66,12 +66,12 @@ def _resolve_mask(mask, causal):
     raise TypeError(f"unsupported attention_mask type {type(mask)}")
 
 
-def attention_grouped(attns, kind, hidden, kv, mask, resid=False):
+def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0):
     """Run G attention operators of the same shape in lock-step (one launch per stage).
 
-    kind: "self" | "causal" | "cross".  Returns out_proj(attn), plus the operator's own
-    query input when `resid` (the post-LN residual of the enclosing block, fused into the
-    out-projection epilogue)."""
+    kind: "self" | "causal" | "cross".  Returns dropout(out_proj(attn), drop_p), plus the
+    operator's own query input when `resid` (the post-LN residual of the enclosing block;
+    residual and dropout ride in the out-projection epilogue)."""
     G = len(attns)
     a0 = attns[0]
     for a in attns:
@@ -85,7 +85,7 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False):
     ts = list(hidden) + (list(kv) if kind == "cross" else []) + params + \
         [a.out_proj.weight for a in attns] + [a.out_proj.bias for a in attns]
     return list(ops.AttentionBlock.apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
-                                         bool(resid), *ts))
+                                         bool(resid), float(drop_p), *ts))
 
 
 class SelfAttention(BaseAttention):

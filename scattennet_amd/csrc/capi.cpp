@@ -15,3 +15,15 @@ extern "C" void sca_set_error(const char* msg) {
 extern "C" const char* sca_last_error(void) { return g_err; }
 
 extern "C" int sca_version(void) { return 1; }
+
+namespace {
+const unsigned long long* g_drop_offset = nullptr;
+}
+
+extern "C" int sca_dropout_offset(const unsigned long long* counter) {
+  g_drop_offset = counter;
+  return SCA_OK;
+}
+
+// read by the launchers (host side) of every dropout-capable kernel
+extern "C" const unsigned long long* sca_drop_offset_ptr(void) { return g_drop_offset; }

@@ -41,3 +41,31 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+
+// Counter-based dropout mask (include/scatten.h, sca_dropout): element e of the tensor
+// dropped by seed `seed` is kept iff mix(mix(e ^ key) + key) >= thr.
+__host__ __device__ __forceinline__ uint32_t sca_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+extern "C" const unsigned long long* sca_drop_offset_ptr(void);
+
+struct DropMask {
+  uint32_t key, thr;
+  float scale;
+  // off: the registered device step counter (sca_dropout_offset) or NULL
+  __device__ __forceinline__ void init(unsigned long long seed, float p, const unsigned long long* off) {
+    if (off) seed += *off * 0x9E3779B97F4A7C15ull;
+    key = sca_mix32((uint32_t)seed ^ sca_mix32((uint32_t)(seed >> 32) + 0x9e3779b9U));
+    thr = (uint32_t)fminf(p * 4294967296.0f, 4294967040.0f);
+    scale = 1.0f / (1.0f - p);
+  }
+  __device__ __forceinline__ float apply(uint32_t e, float v) const {
+    return sca_mix32(sca_mix32(e ^ key) + key) >= thr ? v * scale : 0.0f;
+  }
+};

@@ -33,6 +33,7 @@ struct GemmArgs {
   int nprob;                                    // persistent kernel only:
   int tile_prefix[SCA_GEMM_MAX_PROBLEMS + 1];  // cumulative output tiles (x splitk) per problem
   int tiles_n[SCA_GEMM_MAX_PROBLEMS];           // column tiles per problem
+  const unsigned long long* drop_off;           // dropout step counter (sca_dropout_offset)
 };
 
 // Workgroup tile configuration.
@@ -115,12 +116,18 @@ __device__ __forceinline__ f32x4 read_frag(const float* lds, int r0, int g8, int
   return v;
 }
 
-__device__ __forceinline__ float epilogue(const sca_gemm_problem& P, int m, int n, float v) {
+__device__ __forceinline__ float epilogue(const sca_gemm_problem& P, int m, int n, float v,
+                                          const unsigned long long* drop_off) {
   if (P.bias) v += P.bias[n];
   v *= P.post_scale;
   if (P.epi & SCA_EPI_GELU) {
     P.aux_out[(long)m * P.ldo + n] = v;
     v = gelu_erf(v);
+  }
+  if (P.epi & SCA_EPI_DROPOUT) {
+    DropMask dm;
+    dm.init(P.drop_seed, P.drop_p, drop_off);
+    v = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)n, v);
   }
   if (P.epi & SCA_EPI_DGELU) v *= gelu_erf_grad(P.aux[(long)m * P.ldx + n]);
   if (P.resid) v += P.resid[(long)m * P.ldr + n];
@@ -133,7 +140,9 @@ __device__ __forceinline__ float epilogue(const sca_gemm_problem& P, int m, int 
 // pre-activation) / GELU'; + (resid + C_old).
 template <int RM, int RN>
 __device__ __forceinline__ void epilogue_block(const sca_gemm_problem& P, const f32x16 (&acc)[RM][RN], int mb, int nb,
-                                               int col, int rowh) {
+                                               int col, int rowh, const unsigned long long* drop_off) {
+  DropMask dm;
+  if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, drop_off);
 #pragma unroll
   for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -161,6 +170,7 @@ __device__ __forceinline__ void epilogue_block(const sca_gemm_problem& P, const 
           P.aux_out[(long)m * P.ldo + n] = v;
           v = gelu_erf(v);
         }
+        if (P.epi & SCA_EPI_DROPOUT) v = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)n, v);
         if (P.epi & SCA_EPI_DGELU) v *= gelu_erf_grad(ax[r]);
         P.C[(long)m * P.ldc + n] = v + ex[r];
       }
@@ -313,8 +323,186 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
         }
     return;
   }
-  epilogue_block<RM, RN>(P, acc, m0 + wm, n0 + wn, col, rowh);
+  epilogue_block<RM, RN>(P, acc, m0 + wm, n0 + wn, col, rowh, args.drop_off);
 }
+// ------------------------------------------------------------------------------ LDS-DMA kernel
+// 64x64 tile, 4 waves (32x32 each), BK = 32, an S-stage LDS ring filled by
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write pass), one raw barrier per slice
+// and a counted vmcnt that keeps S-2 slices in flight across it.
+//   k-contiguous operand tile [64 rows][32 k] (128-B rows, 8 rows per 1-KiB DMA piece):
+//     float4 slot s of row r lives at slot s ^ ((r >> 1) & 7) — the swizzle is applied on
+//     the per-lane SOURCE address (the DMA image is lane-linear) and on the fragment read;
+//     conflict-free for the 32x32x2 fragment pattern in all four ds_read_b128 lane groups.
+//   k-major operand tile [32 k][64 cols] (256-B rows, 4 per piece), unswizzled: a fragment
+//     is ds_read_b32 of 32 consecutive floats per half-wave (conflict-free).
+// Requirements (else the register-staged kernel runs): every segment's K (per split-K
+// chunk) a multiple of 32, M and N multiples of 4, one alpha for all segments of a
+// problem (applied to the accumulator).  Rows / columns past M, N are clamped on load and
+// never stored.
+constexpr int GL_BM = 64, GL_BN = 64, GL_BK = 32;
+constexpr int GL_PIECE = 1024;                  // bytes per DMA wave-instruction
+constexpr int GL_OP_BYTES = GL_BM * GL_BK * 4;  // 8 KiB per operand per stage
+
+__device__ __forceinline__ int gl_swz(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ void gl_dma(const float* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void gl_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Per-lane source of this wave's two DMA pieces of one operand tile for K-slice at k0.
+// KC: element (row, k) at base[row*ld + k]; else at base[k*ld + row].
+template <bool KC>
+__device__ __forceinline__ const float* gl_src(const float* base, int ld, int row0, int nrows, int k0, int c,
+                                               int wave, int lane) {
+  if (KC) {
+    const int r = 16 * wave + 8 * c + (lane >> 3);
+    const int ks = (lane & 7) ^ gl_swz(r);
+    return base + (long)min(row0 + r, nrows - 1) * ld + k0 + 4 * ks;
+  } else {
+    const int kr = 4 * (2 * wave + c) + (lane >> 4);
+    return base + (long)(k0 + kr) * ld + min(row0 + 4 * (lane & 15), nrows - 4);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ int gl_dst(int c, int wave) {
+  return KC ? (16 * wave + 8 * c) * 128 : (2 * wave + c) * GL_PIECE;
+}
+
+// 32x32x2 fragment for k-group g (k = 8g + 4h + j, j = 0..3) of rows r0 .. r0+31
+template <bool KC>
+__device__ __forceinline__ f32x4 gl_frag(const char* img, int r0, int g, int lane) {
+  const int r = r0 + (lane & 31), h = lane >> 5;
+  if (KC) return *(const f32x4*)(img + r * 128 + 16 * ((2 * g + h) ^ gl_swz(r)));
+  const float* f = (const float*)img;
+  f32x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = f[(8 * g + 4 * h + j) * 64 + r];
+  return v;
+}
+
+template <int LAYOUT, int S>
+__global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
+  constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
+  constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
+  constexpr int STAGE = 2 * GL_OP_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
+
+  const int splitk = args.splitk;
+  const int pid = bz / splitk;
+  const int ks = bz % splitk;
+  const sca_gemm_problem& P = args.p[pid];
+  const int m0 = by * GL_BM, n0 = bx * GL_BN;
+  if (m0 >= P.M || n0 >= P.N) return;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+
+  // flattened (segment, K-slice) sequence; every chunk is a whole number of slices
+  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
+    seg_kbeg[s] = seg_n[s] = 0;
+    if (s < P.nseg) {
+      int kbeg = 0, kend = P.seg[s].K;
+      if (splitk > 1) {
+        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + GL_BK - 1) / GL_BK * GL_BK;
+        kbeg = ks * chunk;
+        kend = min(P.seg[s].K, kbeg + chunk);
+      }
+      seg_kbeg[s] = kbeg;
+      seg_n[s] = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
+      total += seg_n[s];
+    }
+  }
+  auto dma = [&](int t, int stage) {
+    int s = 0;
+    while (s + 1 < P.nseg && t >= seg_n[s]) { t -= seg_n[s]; ++s; }
+    const sca_gemm_seg& G = P.seg[s];
+    const int k0 = seg_kbeg[s] + t * GL_BK;
+    char* base = smem + stage * STAGE;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      gl_dma(gl_src<A_KC>(G.A, G.lda, m0, P.M, k0, c, wave, lane), base + gl_dst<A_KC>(c, wave));
+      gl_dma(gl_src<B_KC>(G.B, G.ldb, n0, P.N, k0, c, wave, lane), base + GL_OP_BYTES + gl_dst<B_KC>(c, wave));
+    }
+  };
+
+  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && bx == 0;
+  float bsum = 0.f;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < total) dma(i, i);
+  for (int t = 0; t < total; ++t) {
+    // slice t landed for this wave (4 DMA pieces per slice; S-2 younger slices may fly)
+    if (t + S - 2 < total) gl_wait_vm<4 * (S - 2)>();
+    else gl_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of slice t landed; slice t-1 fully read
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+    const char* As = smem + (t % S) * STAGE;
+    const char* Bs = As + GL_OP_BYTES;
+    if (do_bias && threadIdx.x < GL_BM) {
+      const float* af = (const float*)As;  // TN: A image is [32 k][64 m]
+#pragma unroll 8
+      for (int k = 0; k < GL_BK; ++k) bsum += af[k * 64 + threadIdx.x];
+    }
+    f32x4 fa[4], fb[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      fa[g] = gl_frag<A_KC>(As, wm, g, lane);
+      fb[g] = gl_frag<B_KC>(Bs, wn, g, lane);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
+  }
+
+  const float alpha = P.seg[0].alpha;
+  const int col = lane & 31;
+  const int rowh = 4 * (lane >> 5);
+  if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
+    if (splitk > 1)
+      args.ws[(long)gridDim.z * P.M * P.N + (long)bz * P.M + m0 + threadIdx.x] = bsum * alpha;
+    else
+      P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
+  }
+  if (alpha != 1.f) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] *= alpha;
+  }
+  if (splitk > 1) {
+    float* slab = args.ws + (long)bz * P.M * P.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + rowh;
+      const int n = n0 + wn + col;
+      if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[r];
+    }
+    return;
+  }
+  const f32x16 accs[1][1] = {{acc}};
+  epilogue_block<1, 1>(P, accs, m0 + wm, n0 + wn, col, rowh, args.drop_off);
+}
+
 // ------------------------------------------------------------------------------ persistent
 // One output tile of the persistent kernel: integers only (wave-uniform).  Pointers and
 // leading dimensions are re-read from the kernel arguments (scalar loads) at each fetch,
@@ -482,7 +670,7 @@ __global__ __launch_bounds__(C::NT) void gemm_persistent_kernel(const GemmArgs a
               if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[i][j][r];
             }
       } else {
-        epilogue_block<RM, RN>(P, acc, cur.m0 + wm, cur.n0 + wn, col, rowh);
+        epilogue_block<RM, RN>(P, acc, cur.m0 + wm, cur.n0 + wn, col, rowh, args.drop_off);
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -522,7 +710,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args,
   const float* slab = args.ws + (long)blockIdx.y * args.splitk * MN + e;
   float v = 0.f;
   for (int s = 0; s < args.splitk; ++s) v += slab[s * MN];
-  P.C[(long)m * P.ldc + n] = epilogue(P, m, n, v);
+  P.C[(long)m * P.ldc + n] = epilogue(P, m, n, v, args.drop_off);
 }
 
 int pick_grid(int tiles, int max_per_cu) {
@@ -588,10 +776,32 @@ bool persistent_ok(const GemmArgs& a, int nprob) {
   return true;
 }
 
+// the LDS-DMA kernel's shape requirements (see gemm_glds_kernel)
+bool glds_ok(const GemmArgs& a, int nprob) {
+  for (int i = 0; i < nprob; ++i) {
+    const sca_gemm_problem& P = a.p[i];
+    if ((P.M & 3) || (P.N & 3)) return false;
+    for (int s = 0; s < P.nseg; ++s)
+      if ((P.seg[s].K % GL_BK) || P.seg[s].alpha != P.seg[0].alpha) return false;
+  }
+  return true;
+}
+
+template <int LAYOUT, int S>
+int launch_glds(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
+  hipLaunchKernelGGL((gemm_glds_kernel<LAYOUT, S>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  if (tile > 10 && !persistent_ok(a, nprob)) tile = 1;
+  if (tile > 10 && tile < 20 && !persistent_ok(a, nprob)) tile = 1;
+  if (tile >= 20 && !glds_ok(a, nprob)) tile = LAYOUT == SCA_GEMM_TN ? 5 : (LAYOUT == SCA_GEMM_NN ? 7 : 1);
   switch (tile) {
+    case 20: return launch_glds<LAYOUT, 3>(a, nprob, maxM, maxN, st);
+    case 21: return launch_glds<LAYOUT, 2>(a, nprob, maxM, maxN, st);
+    case 22: return launch_glds<LAYOUT, 4>(a, nprob, maxM, maxN, st);
     case 11: return launch_persistent<LAYOUT, T1>(a, nprob, st);
     case 12: return launch_persistent<LAYOUT, T2>(a, nprob, st);
     case 13: return launch_persistent<LAYOUT, T3>(a, nprob, st);
@@ -613,20 +823,20 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
 int g_tile_override[3] = {0, 0, 0};
 
 // Tile heuristic (measured with tools/gemm_bench.py at the workload's shapes, see
-// DESIGN.md): 64x64 / 4 waves for the forward (NT), 128x64 / 8 waves for dX (NN), the
-// single-buffered 64x64 (8 workgroups per CU) for the split-K weight gradients (TN).
+// DESIGN.md): the 3-stage LDS-DMA 64x64 kernel wins every layout; ineligible shapes fall
+// back to 64x64 / 4 waves (NT), 128x64 / 8 waves (NN), single-buffered 64x64 (TN).
 int pick_tile(int layout, long tiles64, int splitk) {
   if (g_tile_override[layout]) return g_tile_override[layout];
   (void)splitk;
-  if (layout == SCA_GEMM_NN && tiles64 >= 512) return 7;
-  if (layout == SCA_GEMM_TN) return 5;
-  return 1;
+  (void)tiles64;
+  return 20;  // LDS-DMA kernel; launch_tile falls back per layout when a shape is not eligible
 }
 
 }  // namespace
 
 extern "C" int sca_gemm_tile_override(int layout, int tile) {
-  if (layout < 0 || layout > 2 || tile < 0 || (tile > kNumTiles && (tile < 11 || tile > 16))) return SCA_ERR_ARG;
+  if (layout < 0 || layout > 2 || tile < 0 || (tile > kNumTiles && (tile < 11 || tile > 16) && (tile < 20 || tile > 22)))
+    return SCA_ERR_ARG;
   g_tile_override[layout] = tile;
   return SCA_OK;
 }
@@ -643,6 +853,7 @@ extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, in
   GemmArgs a;
   a.splitk = splitk;
   a.ws = workspace;
+  a.drop_off = sca_drop_offset_ptr();
   int maxM = 0, maxN = 0;
   for (int i = 0; i < nprob; ++i) {
     const sca_gemm_problem& P = probs[i];
@@ -666,6 +877,10 @@ extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, in
     if ((P.epi & SCA_EPI_GELU) && !P.aux_out) { sca_set_error("sca_gemm: GELU needs aux_out"); return SCA_ERR_ARG; }
     if ((P.epi & SCA_EPI_DGELU) && !P.aux) { sca_set_error("sca_gemm: DGELU needs aux"); return SCA_ERR_ARG; }
     if (P.bias_grad && layout != SCA_GEMM_TN) { sca_set_error("sca_gemm: bias_grad only with TN"); return SCA_ERR_ARG; }
+    if ((P.epi & SCA_EPI_DROPOUT) && !(P.drop_p >= 0.f && P.drop_p < 1.f)) {
+      sca_set_error("sca_gemm: drop_p must be in [0, 1)");
+      return SCA_ERR_ARG;
+    }
     if (splitk > 1 && (P.nseg != 1 || P.M != probs[0].M || P.N != probs[0].N)) {
       sca_set_error("sca_gemm: split-K needs one segment and equal M,N");
       return SCA_ERR_ARG;

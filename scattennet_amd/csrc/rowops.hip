@@ -15,6 +15,7 @@ struct LnFwdArgs {
   sca_ln_fwd_problem p[SCA_LN_MAX_PROBLEMS];
   int rows, N, r_mod, r_off;
   float eps;
+  const unsigned long long* drop_off;
 };
 struct LnBwdArgs {
   sca_ln_bwd_problem p[SCA_LN_MAX_PROBLEMS];
@@ -104,6 +105,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const LnFwdArgs a) {
     if (P.post) o += t[i];
     if (P.act == SCA_ACT_RELU) o = fmaxf(o, 0.f);
     v[i] = o;
+  }
+  if (P.drop_p > 0.f) {  // embedding dropout (keypoint_module.py:164-165)
+    DropMask dm;
+    dm.init(P.drop_seed, P.drop_p, a.drop_off);
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = dm.apply((uint32_t)row * (uint32_t)N + (uint32_t)RM::col(lane, i), v[i]);
   }
   store_row<NV>(P.y + (long)row * N, v, lane, N);
   if (lane == 0) {
@@ -473,6 +480,29 @@ __global__ __launch_bounds__(256) void coord_map_bwd_kp_kernel(const MapBwdArgs 
   }
 }
 
+// ------------------------------------------------------------------------------ dropout
+struct DropArgs {
+  sca_dropout_problem p[SCA_DROPOUT_MAX_PROBLEMS];
+  long n;
+  float prob;
+  const unsigned long long* drop_off;
+};
+
+__global__ __launch_bounds__(256) void dropout_kernel(const DropArgs a) {
+  const sca_dropout_problem& P = a.p[blockIdx.y];
+  DropMask dm;
+  dm.init(P.seed, a.prob, a.drop_off);
+  const long n4 = a.n >> 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4 v = ld4(P.x + 4 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = dm.apply((uint32_t)(4 * i + j), v[j]);
+    st4(P.y + 4 * i, v);
+  }
+  for (long e = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; e < a.n; e += (long)gridDim.x * 256)
+    P.y[e] = dm.apply((uint32_t)e, P.x[e]);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------ C ABI
@@ -486,8 +516,15 @@ extern "C" int sca_layernorm_fwd(int nprob, const sca_ln_fwd_problem* probs, int
   }
   if (rows == 0) return SCA_OK;
   LnFwdArgs a;
-  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  for (int i = 0; i < nprob; ++i) {
+    a.p[i] = probs[i];
+    if (!(probs[i].drop_p >= 0.f && probs[i].drop_p < 1.f) || (probs[i].drop_p > 0.f && probs[i].act != SCA_ACT_NONE)) {
+      sca_set_error("sca_layernorm_fwd: drop_p must be in [0, 1) and needs act == SCA_ACT_NONE");
+      return SCA_ERR_ARG;
+    }
+  }
   a.rows = rows; a.N = N; a.r_mod = r_mod; a.r_off = r_off; a.eps = eps;
+  a.drop_off = sca_drop_offset_ptr();
   dim3 grid((rows + 3) / 4, nprob);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (N % 256 == 0 ? N / 256 : 0) {
@@ -690,5 +727,30 @@ extern "C" int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* pro
     r.S = a.nchunk; r.I = 1; r.N = NK; r.accumulate = 0; r.stride_s = NK; r.stride_i = 0;
     if (launch_reduce(r, 2, st) != SCA_OK) { sca_set_error("sca_coord_map_bwd: reduce launch failed"); return SCA_ERR_LAUNCH; }
   }
+  return SCA_OK;
+}
+
+extern "C" int sca_dropout(int nprob, const sca_dropout_problem* probs, long rows, int cols, float p, void* stream) {
+  if (nprob < 1 || nprob > SCA_DROPOUT_MAX_PROBLEMS || rows < 0 || cols < 0 || !(p >= 0.f && p < 1.f)) {
+    sca_set_error("sca_dropout: bad arguments (p must be in [0, 1))");
+    return SCA_ERR_ARG;
+  }
+  DropArgs a;
+  for (int i = 0; i < nprob; ++i) {
+    if (!probs[i].x || !probs[i].y || (reinterpret_cast<uintptr_t>(probs[i].x) & 15) ||
+        (reinterpret_cast<uintptr_t>(probs[i].y) & 15)) {
+      sca_set_error("sca_dropout: x / y must be non-null and 16-byte aligned");
+      return SCA_ERR_ARG;
+    }
+    a.p[i] = probs[i];
+  }
+  a.n = rows * (long)cols;
+  a.prob = p;
+  a.drop_off = sca_drop_offset_ptr();
+  if (a.n == 0) return SCA_OK;
+  const long want = (a.n / 4 + 255) / 256;
+  const int blocks = (int)(want < 2048 ? (want > 0 ? want : 1) : 2048);
+  hipLaunchKernelGGL(dropout_kernel, dim3(blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_dropout: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

@@ -3,7 +3,7 @@ the cross-stream fusion of the left / right / body stream encodings (BASELINE co
 import torch.nn as nn
 
 from . import ops
-from .layers import layernorm_grouped
+from .layers import drop_p, layernorm_grouped
 
 
 def _lin(layers, xs, gelu=False, resid=None):
@@ -35,16 +35,19 @@ class CoordinatesFusion(nn.Module):
         self.drop_rate = drop_rate
 
     def forward(self, left_embed, right_embed, body_embed):
-        if self.training and self.drop_rate > 0:
-            raise NotImplementedError("CoordinatesFusion dropout > 0 in training mode is not implemented "
-                                      "(use eval() or drop_rate=0)")
+        p = drop_p([self], "drop_rate")
         lo, ro, bo = _lin([self.left_se, self.right_se, self.body_se], [left_embed, right_embed, body_embed],
                           gelu=True)
         attn = ops.SoftmaxRows.apply(ops.ClipMatmul.apply(True, ro, lo))
+        if p > 0:  # fusion.py:48
+            attn = ops.dropout_grouped([attn], p)[0]
         fuse = ops.ClipMatmul.apply(False, attn, bo)
         fuse = _lin([self.out_proj], [fuse])
         fuse = layernorm_grouped([self.norm], fuse)[0]
-        return self.inverted_res(fuse)
+        fuse = self.inverted_res(fuse)
+        if p > 0:  # fusion.py:54
+            fuse = ops.dropout_grouped([fuse], p)[0]
+        return fuse
 
 
 class InvertedResidual(nn.Module):

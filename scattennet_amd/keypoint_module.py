@@ -10,8 +10,8 @@ from torch import nn
 
 from . import ops
 from .attention import CrossAttention, SelfAttention, SelfCausalAttention, attention_grouped
-from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, check_dropout,
-                     coordinate_mapping_grouped, ffn_grouped, layernorm_grouped, pos_embed_layernorm_grouped)
+from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, coordinate_mapping_grouped, drop_p,
+                     ffn_grouped, layernorm_grouped, pos_embed_layernorm_grouped)
 from .residual import ResidualNetwork, residual_network_grouped
 from .utils import key_padding_mask
 
@@ -46,9 +46,8 @@ class CoordinateAttention(nn.Module):
 def coordinate_attention_grouped(blocks, xs, mask):
     """h = LN(x + Attn(x)); self type: h = LN(h + FFN(h))  (keypoint_module.py:61-80).
     The residual adds ride in the out-projection / fc2 epilogues."""
-    check_dropout(blocks)
     kind = "self" if blocks[0].attn_type == "self_attn" else "causal"
-    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=True)
+    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=True, drop_p=drop_p(blocks))
     h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
     if kind == "self":
         h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
@@ -74,8 +73,7 @@ class CoordinatesMerge(nn.Module):
 
 
 def coordinates_merge_grouped(blocks, ys, xs, mask):
-    check_dropout(blocks)
-    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True)
+    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True, drop_p=drop_p(blocks))
     h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
     h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
     return layernorm_grouped([b.last_layer_norm for b in blocks], h)
@@ -111,13 +109,13 @@ def sca_grouped(scas, xs, ys, attention_mask):
 
     Data dependency (keypoint_module.py:176-187): every merge layer reads the FINAL x-stream
     map, so the L self layers run first, then L x (causal, merge)."""
-    check_dropout(scas)
+    p = drop_p(scas)
     if attention_mask is None:
         raise AttributeError("'NoneType' object has no attribute 'size'")  # reference: mask.size()
     x_self = scas[0].x_self
     se, ce = (xs, ys) if x_self else (ys, xs)
-    se = pos_embed_layernorm_grouped([m.self_pos_embed for m in scas], [m.first_self_norm for m in scas], se)
-    ce = pos_embed_layernorm_grouped([m.causal_pos_embed for m in scas], [m.first_causal_norm for m in scas], ce)
+    se = pos_embed_layernorm_grouped([m.self_pos_embed for m in scas], [m.first_self_norm for m in scas], se, p)
+    ce = pos_embed_layernorm_grouped([m.causal_pos_embed for m in scas], [m.first_causal_norm for m in scas], ce, p)
     self_mask = key_padding_mask(attention_mask)  # model/utils.py:3-12
     causal_mask = key_padding_mask(attention_mask, causal=True)  # model/utils.py:15-28
     cross_mask = self_mask  # create_attention_mask(tgt_len=T) — same key padding

@@ -21,32 +21,37 @@ class LearningPositionEmbedding(nn.Embedding):
         return inputs_embeds + self.weight[self.offset:self.offset + seq_len][None]
 
 
-def pos_embed_layernorm_grouped(tables, norms, xs):
-    """G-way fused  LayerNorm(x + table[2:T+2])  (keypoint_module.py:154-162)."""
-    return list(ops.LayerNormAdd.apply(len(xs), norms[0].eps, True, False, 0, *xs, *[e.weight for e in tables],
-                                       *[n.weight for n in norms], *[n.bias for n in norms]))
+def pos_embed_layernorm_grouped(tables, norms, xs, drop_p=0.0):
+    """G-way fused  dropout(LayerNorm(x + table[2:T+2]))  (keypoint_module.py:154-165)."""
+    return list(ops.LayerNormAdd.apply(len(xs), norms[0].eps, True, False, 0, float(drop_p), *xs,
+                                       *[e.weight for e in tables], *[n.weight for n in norms],
+                                       *[n.bias for n in norms]))
 
 
 def layernorm_grouped(norms, xs, post=None, relu=False):
     """G-way y = act(LayerNorm(x) + post)."""
     extra = list(post) if post is not None else []
-    return list(ops.LayerNormAdd.apply(len(xs), norms[0].eps, False, post is not None, 1 if relu else 0, *xs,
+    return list(ops.LayerNormAdd.apply(len(xs), norms[0].eps, False, post is not None, 1 if relu else 0, 0.0, *xs,
                                        *extra, *[n.weight for n in norms], *[n.bias for n in norms]))
 
 
-def check_dropout(mods, attr="dropout"):
-    for m in mods:
-        if m.training and getattr(m, attr) > 0:
-            raise NotImplementedError("dropout > 0 in training mode is not implemented on the HIP path "
-                                      "(use eval() or dropout=0)")
+def drop_p(mods, attr="dropout"):
+    """The dropout probability a group of same-config modules applies now: their `attr` in
+    training mode, 0 in eval mode (F.dropout(..., training=self.training))."""
+    ps = {float(getattr(m, attr)) if m.training else 0.0 for m in mods}
+    if len(ps) != 1:
+        raise ValueError("grouped modules must share dropout and training mode")
+    p = ps.pop()
+    if not 0.0 <= p < 1.0:
+        raise ValueError(f"dropout probability has to be in [0, 1), but got {p}")
+    return p
 
 
 def ffn_grouped(ffns, xs, residual=True):
     """G-way FFN (layers.py:104-108); with `residual` the enclosing block's residual add is
     fused (y = FFN(x) + x, keypoint_module.py:71-72 / :108-109)."""
-    check_dropout(ffns)
     G = len(xs)
-    return list(ops.FeedForwardResidual.apply(G, residual, *xs, *[f.fc1.weight for f in ffns],
+    return list(ops.FeedForwardResidual.apply(G, residual, drop_p(ffns), *xs, *[f.fc1.weight for f in ffns],
                                               *[f.fc1.bias for f in ffns], *[f.fc2.weight for f in ffns],
                                               *[f.fc2.bias for f in ffns]))
 

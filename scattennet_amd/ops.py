@@ -76,10 +76,87 @@ def _seg(A, B, lda, ldb, K, alpha=1.0):
 
 
 def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=0, aux=None, ldx=0,
-          aux_out=None, ldo=0, bias_grad=None, bias_grad_scale=1.0):
+          aux_out=None, ldo=0, bias_grad=None, bias_grad_scale=1.0, drop=None):
+    """drop: None or (seed, p) -> the DROPOUT epilogue with that seed's mask."""
     s = list(segs) + [_NOSEG] * (3 - len(segs))
+    seed, p = (0, 0.0) if drop is None else drop
+    if drop is not None:
+        epi |= L.EPI_DROPOUT
     return L.GemmProblem((L.GemmSeg * 3)(*s), len(segs), M, N, C.data_ptr(), ldc, epi, ptr(bias), post_scale,
-                         ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo, ptr(bias_grad), bias_grad_scale)
+                         ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo, ptr(bias_grad), bias_grad_scale,
+                         seed, p)
+
+
+# --------------------------------------------------------------------------- dropout
+_SEED_SOURCE = None  # tests install a deterministic, logging source (tests/test_dropout.py)
+
+
+_COUNTER = None
+
+
+def dropout_counter():
+    """The device step counter every dropout mask reads (include/scatten.h,
+    sca_dropout_offset): incrementing it inside a captured graph step (advance_dropout)
+    gives every replay fresh masks.  One per process (one GPU per process)."""
+    global _COUNTER
+    if _COUNTER is None:
+        _COUNTER = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+        L.check(L.lib().sca_dropout_offset(ptr(_COUNTER)), "sca_dropout_offset")
+    return _COUNTER
+
+
+def advance_dropout():
+    """Next training step's masks (capture-safe: a device-side increment)."""
+    dropout_counter().add_(1)
+
+
+def dropout_seeds(n):
+    """n fresh 64-bit dropout seeds, one mask each.  Drawn from torch's CPU generator, so
+    torch.manual_seed() makes a training run reproducible, as with F.dropout."""
+    dropout_counter()
+    if _SEED_SOURCE is not None:
+        return [int(v) for v in _SEED_SOURCE(n)]
+    return [int(v) for v in torch.randint(0, 2 ** 63 - 1, (n,), dtype=torch.int64)]
+
+
+def dropout_apply(items, p):
+    """items: [(x, y, seed)] same-shaped contiguous fp32 tensors; y = dropout_seed(x) (y may be x)."""
+    if not items:
+        return
+    x0 = items[0][0]
+    cols = x0.shape[-1] if x0.dim() else 1
+    rows = x0.numel() // max(cols, 1)
+    for c in range(0, len(items), L.DROPOUT_MAX_PROBLEMS):
+        chunk = items[c:c + L.DROPOUT_MAX_PROBLEMS]
+        arr = (L.DropoutProblem * len(chunk))(*[L.DropoutProblem(x.data_ptr(), y.data_ptr(), sd) for x, y, sd in chunk])
+        L.check(L.lib().sca_dropout(len(chunk), arr, rows, cols, float(p), L.stream_handle()), "sca_dropout")
+
+
+class Dropout(Function):
+    """F.dropout(x, p, training=True) for G same-shaped tensors (one seed each); the backward
+    regenerates each mask from its seed."""
+
+    @staticmethod
+    def forward(ctx, p, *xs):
+        xs = _contig(xs)
+        L.require_device(*xs)
+        seeds = dropout_seeds(len(xs))
+        ys = [torch.empty_like(x) for x in xs]
+        dropout_apply([(x, y, sd) for x, y, sd in zip(xs, ys, seeds)], p)
+        ctx.p, ctx.seeds = p, seeds
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        dys = _contig(dys)
+        dxs = [torch.empty_like(d) for d in dys]
+        dropout_apply([(d, o, sd) for d, o, sd in zip(dys, dxs, ctx.seeds)], ctx.p)
+        return (None,) + tuple(dxs)
+
+
+def dropout_grouped(xs, p):
+    """G-way F.dropout in training mode (p > 0)."""
+    return list(Dropout.apply(float(p), *xs))
 
 
 def gemm(layout, probs, splitk=1, ws=None):
@@ -248,7 +325,7 @@ def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v):
     return o, sm, sl
 
 
-def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, dout):
+def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, dout, dq_scale=1.0, dv_scale=1.0):
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
@@ -262,7 +339,7 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
             L.AttnBwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
                              dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
                              ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
-                             delta[g].data_ptr(), 1.0, 1.0) for g in gs])
+                             delta[g].data_ptr(), dq_scale, dv_scale) for g in gs])
         fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
         with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
             L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
@@ -283,7 +360,7 @@ class AttentionBlock(Function):
     into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, *ts):
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, *ts):
         cross = kind == "cross"
         causal = kind == "causal"
         xq = _contig(ts[:G])
@@ -309,9 +386,13 @@ class AttentionBlock(Function):
         gemm(L.GEMM_NT, probs)
         o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v)
         ys = [torch.empty_like(x) for x in xq]
+        # y = x + dropout(o Wo^T + bo)  (keypoint_module.py:63-65 / :99-101) in one epilogue
+        seeds = dropout_seeds(G) if drop_p > 0 else [None] * G
         gemm(L.GEMM_NT, [_prob([_seg(_flat(o[g]), Wo[g], d, d, d)], ys[g], B * T, d, d, bias=bo[g],
-                               resid=_flat(xq[g]) if has_resid else None, ldr=d) for g in range(G)])
+                               resid=_flat(xq[g]) if has_resid else None, ldr=d,
+                               drop=(seeds[g], drop_p) if drop_p > 0 else None) for g in range(G)])
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
+        ctx.drop_p, ctx.seeds = drop_p, seeds
         ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
                               *sm, *sl)
         return tuple(ys)
@@ -336,10 +417,17 @@ class AttentionBlock(Function):
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
         dys = _contig(_zeros_for_none(dys, xq))
-        # out-projection: dO = dY Wo
+        dyo = dys  # gradient of the out-projection output: the dropout mask applied to dY
+        if ctx.drop_p > 0:
+            dyo = [torch.empty_like(t) for t in dys]
+            dropout_apply([(dys[g], dyo[g], ctx.seeds[g]) for g in range(G)], ctx.drop_p)
+        # out-projection: dO = dY' Wo
         do = [torch.empty_like(t) for t in o]
-        gemm(L.GEMM_NN, [_prob([_seg(_flat(dys[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
-        dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do)
+        gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
+        # dq comes back pre-multiplied by the q scale and dv by alpha_v, so that every GEMM below
+        # runs with unit segment scales: dX = dq' Wq + dk Wk + dv' Wv, dWq = dq'^T x, ...
+        dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do,
+                               dq_scale=scale, dv_scale=av)
         # input gradients (residual gradient fused as the epilogue's resid term)
         dxq, dxkv, probs = [], [], []
         for g in range(G):
@@ -349,11 +437,11 @@ class AttentionBlock(Function):
             gx = torch.empty_like(xq[g])
             if cross:
                 gkv = torch.empty_like(xkv[g])
-                probs.append(_prob([_seg(dqf, Wq, d, d, d, scale)], gx, B * T, d, d, resid=r, ldr=d))
-                probs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d, av)], gkv, B * Tk, d, d))
+                probs.append(_prob([_seg(dqf, Wq, d, d, d)], gx, B * T, d, d, resid=r, ldr=d))
+                probs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
                 dxkv.append(gkv)
             else:
-                probs.append(_prob([_seg(dqf, Wq, d, d, d, scale), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
+                probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
                                    gx, B * T, d, d, resid=r, ldr=d))
             dxq.append(gx)
         gemm(L.GEMM_NN, probs)
@@ -362,9 +450,9 @@ class AttentionBlock(Function):
         for g in range(G):
             Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
             xf, kf = _flat(xq[g]), _flat(xkv[g])
-            items += [(_flat(dq[g]), xf, scale, Wq, bq is not None), (_flat(dk[g]), kf, 1.0, Wk, bk is not None),
-                      (_flat(dv[g]), kf, av, Wv, bv is not None, 1.0),
-                      (_flat(dys[g]), _flat(o[g]), 1.0, Wo[g], bo[g] is not None)]
+            items += [(_flat(dq[g]), xf, 1.0, Wq, bq is not None), (_flat(dk[g]), kf, 1.0, Wk, bk is not None),
+                      (_flat(dv[g]), kf, 1.0, Wv, bv is not None, 1.0 / av),
+                      (_flat(dyo[g]), _flat(o[g]), 1.0, Wo[g], bo[g] is not None)]
         wg = weight_grads(items)
         dW, dWo, dbo = [], [], []
         for g in range(G):
@@ -372,7 +460,7 @@ class AttentionBlock(Function):
                 dW += list(wg[4 * g + j])
             dWo.append(wg[4 * g + 3][0])
             dbo.append(wg[4 * g + 3][1])
-        return (None,) * 8 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + tuple(dbo)
+        return (None,) * 9 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + tuple(dbo)
 
 
 # --------------------------------------------------------------------------- Linear (+ residual)
@@ -426,7 +514,7 @@ class FeedForwardResidual(Function):
     backward's dX GEMM of fc2 applies GELU' in its epilogue."""
 
     @staticmethod
-    def forward(ctx, G, has_r, *ts):
+    def forward(ctx, G, has_r, drop_p, *ts):
         x = _contig(ts[:G])
         W1, b1, W2, b2 = ts[G:2 * G], ts[2 * G:3 * G], ts[3 * G:4 * G], ts[4 * G:5 * G]
         L.require_device(*x)
@@ -435,12 +523,17 @@ class FeedForwardResidual(Function):
         F_ = W1[0].shape[0]
         zs = [x[0].new_empty(M, F_) for _ in range(G)]
         acts = [x[0].new_empty(M, F_) for _ in range(G)]
+        # layers.py:104-107: dropout(GELU(fc1 x)) -> fc2 -> dropout (+ x), each dropout fused
+        s1 = dropout_seeds(G) if drop_p > 0 else [None] * G
+        s2 = dropout_seeds(G) if drop_p > 0 else [None] * G
         gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
-                               epi=L.EPI_GELU, aux_out=zs[g], ldo=F_) for g in range(G)])
+                               epi=L.EPI_GELU, aux_out=zs[g], ldo=F_,
+                               drop=(s1[g], drop_p) if drop_p > 0 else None) for g in range(G)])
         ys = [torch.empty_like(x[g]) for g in range(G)]
         gemm(L.GEMM_NT, [_prob([_seg(acts[g], W2[g], F_, F_, F_)], ys[g], M, d, d, bias=b2[g],
-                               resid=_flat(x[g]) if has_r else None, ldr=d) for g in range(G)])
-        ctx.G, ctx.has_r = G, has_r
+                               resid=_flat(x[g]) if has_r else None, ldr=d,
+                               drop=(s2[g], drop_p) if drop_p > 0 else None) for g in range(G)])
+        ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2 = G, has_r, drop_p, s1, s2
         ctx.save_for_backward(*x, *W1, *W2, *zs, *acts)
         return tuple(ys)
 
@@ -453,20 +546,25 @@ class FeedForwardResidual(Function):
         B, T, d = x[0].shape
         M = B * T
         F_ = W1[0].shape[0]
+        p = ctx.drop_p
+        dyo = dys  # gradient of fc2's output (second dropout's mask applied)
+        if p > 0:
+            dyo = [torch.empty_like(t) for t in dys]
+            dropout_apply([(dys[g], dyo[g], ctx.s2[g]) for g in range(G)], p)
         dz = [x[0].new_empty(M, F_) for _ in range(G)]
-        # dz = (dy W2) * gelu'(z)
-        gemm(L.GEMM_NN, [_prob([_seg(_flat(dys[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
-                               aux=zs[g], ldx=F_) for g in range(G)])
+        # dz = mask1 * (dy' W2) * gelu'(z)
+        gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
+                               aux=zs[g], ldx=F_, drop=(ctx.s1[g], p) if p > 0 else None) for g in range(G)])
         # dx = dz W1 + dy   (residual)
         dx = [torch.empty_like(x[g]) for g in range(G)]
         gemm(L.GEMM_NN, [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
                                resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)])
-        items = [(_flat(dys[g]), acts[g], 1.0, W2[g], True) for g in range(G)] + \
+        items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], True) for g in range(G)] + \
                 [(dz[g], _flat(x[g]), 1.0, W1[g], True) for g in range(G)]
         wg = weight_grads(items)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
-        return (None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
+        return (None, None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
             tuple(w for w, _ in dW2) + tuple(b for _, b in dW2)
 
 
@@ -480,7 +578,7 @@ class LayerNormAdd(Function):
        or ReLU alone (norm1 -> relu, :32-33)."""
 
     @staticmethod
-    def forward(ctx, G, eps, pos_table, has_post, act, *ts):
+    def forward(ctx, G, eps, pos_table, has_post, act, drop_p, *ts):
         x = _contig(ts[:G])
         o = G
         tab = ts[o:o + G] if pos_table else [None] * G
@@ -501,15 +599,18 @@ class LayerNormAdd(Function):
         ys = [torch.empty_like(t) for t in x]
         means = [x[0].new_empty(rows) for _ in range(G)]
         rstds = [x[0].new_empty(rows) for _ in range(G)]
+        seeds = dropout_seeds(G) if drop_p > 0 else [0] * G
         for c in range(0, G, L.LN_MAX_PROBLEMS):
             gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
             arr = (L.LnFwdProblem * len(gs))(*[L.LnFwdProblem(x[g].data_ptr(), ptr(tab[g]), gam[g].data_ptr(),
                                                                 bet[g].data_ptr(), ptr(post[g]), ys[g].data_ptr(),
-                                                                means[g].data_ptr(), rstds[g].data_ptr(), act)
+                                                                means[g].data_ptr(), rstds[g].data_ptr(), act,
+                                                                seeds[g], float(drop_p))
                                                  for g in gs])
             L.check(L.lib().sca_layernorm_fwd(len(gs), arr, rows, N, r_mod, r_off, eps, L.stream_handle()),
                     "sca_layernorm_fwd")
         ctx.G, ctx.pos, ctx.has_post, ctx.act, ctx.r_mod, ctx.r_off = G, pos_table, has_post, act, r_mod, r_off
+        ctx.drop_p, ctx.seeds = drop_p, seeds
         ctx.save_for_backward(*x, *(tab if pos_table else []), *gam, *means, *rstds, *(ys if act else []))
         return tuple(ys)
 
@@ -524,6 +625,10 @@ class LayerNormAdd(Function):
         gam, means, rstds = sv[o:o + G], sv[o + G:o + 2 * G], sv[o + 2 * G:o + 3 * G]
         ys = sv[o + 3 * G:o + 4 * G] if act else [None] * G
         dys = _contig(_zeros_for_none(dys, x))
+        if ctx.drop_p > 0:  # gradient of the pre-dropout LayerNorm output
+            dd = [torch.empty_like(t) for t in dys]
+            dropout_apply([(dys[g], dd[g], ctx.seeds[g]) for g in range(G)], ctx.drop_p)
+            dys = dd
         N = x[0].shape[-1]
         rows = x[0].numel() // N
         nblk = L.lib().sca_layernorm_bwd_blocks(rows)
@@ -547,7 +652,7 @@ class LayerNormAdd(Function):
             dtab = [torch.zeros_like(t) for t in tab]
             # d table[t + 2] = sum_b dv[b, t]
             reduce_rows([(dx[g], dtab[g][2:], 1.0) for g in range(G)], B, T, N, T * N, N)
-        return (None,) * 5 + tuple(dx) + tuple(dtab) + (tuple(dpost) if ctx.has_post else ()) + \
+        return (None,) * 6 + tuple(dx) + tuple(dtab) + (tuple(dpost) if ctx.has_post else ()) + \
             tuple(dg) + tuple(db)
 
 

@@ -35,12 +35,43 @@ def test_library_exports_every_declared_symbol():
     assert set(_declared()) - {"sca_set_error"} <= set(_lib.EXPORTS), set(_declared()) - set(_lib.EXPORTS)
 
 
-def test_struct_sizes_match_header_layout():
-    """ctypes mirrors of the C structs: pointer-aligned sizes the kernels rely on."""
+_STRUCTS = {  # C struct in include/scatten.h -> ctypes mirror in scattennet_amd/_lib.py
+    "sca_gemm_seg": "GemmSeg", "sca_gemm_problem": "GemmProblem", "sca_attn_fwd_problem": "AttnFwdProblem",
+    "sca_attn_bwd_problem": "AttnBwdProblem", "sca_ln_fwd_problem": "LnFwdProblem",
+    "sca_ln_bwd_problem": "LnBwdProblem", "sca_pool_problem": "PoolProblem", "sca_softmax_problem": "SoftmaxProblem",
+    "sca_gelu_bwd_problem": "GeluBwdProblem", "sca_reduce_problem": "ReduceProblem",
+    "sca_coord_map_problem": "CoordMapProblem", "sca_coord_map_bwd_problem": "CoordMapBwdProblem",
+    "sca_dropout_problem": "DropoutProblem",
+}
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror has the C struct's size and field offsets (compiled with gcc from
+    the header itself)."""
+    import shutil
+    import subprocess
     from scattennet_amd import _lib as L
-    assert ctypes.sizeof(L.GemmSeg) == 32
-    assert ctypes.sizeof(L.GemmProblem) % 8 == 0
-    assert ctypes.sizeof(L.AttnFwdProblem) == 64
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "scatten.h"', "int main(void) {"]
+    for cs, py in _STRUCTS.items():
+        lines.append(f'printf("{py} size %zu\\n", sizeof({cs}));')
+        for f, _ in getattr(L, py)._fields_:
+            cf = {"inp": "in"}.get(f, f)  # C field names that are Python keywords
+            lines.append(f'printf("{py}.{f} %zu\\n", offsetof({cs}, {cf}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = dict(line.rsplit(" ", 1) for line in out if line)
+    for cs, py in _STRUCTS.items():
+        cls = getattr(L, py)
+        assert int(got[f"{py} size"]) == ctypes.sizeof(cls), py
+        for f, _ in cls._fields_:
+            assert int(got[f"{py}.{f}"]) == getattr(cls, f).offset, (py, f)
 
 
 def test_cpu_tensors_are_rejected():
