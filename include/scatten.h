@@ -100,6 +100,13 @@ typedef struct {
  * reduces them in a second launch in fixed order (deterministic).                       */
 int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
              void* stream);
+/* The two launches of a split-K sca_gemm issued separately (same arguments): the GEMM
+ * writing the slabs, then the fixed-order reduction + epilogue (lets a caller time them
+ * apart, or put work between them).  sca_gemm_partial with splitk == 1 is sca_gemm.     */
+int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                     void* stream);
+int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                    void* stream);
 
 /* Tuning knob: force the workgroup tile of one layout (0 = built-in heuristic,
  * 1 = 64x64, 2 = 128x64, 3 = 64x128, 4 = 128x128).  Process-global; not thread-safe.   */

@@ -97,6 +97,8 @@ class CoordMapBwdProblem(ctypes.Structure):
 
 EXPORTS = {
     "sca_gemm": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "sca_gemm_partial": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "sca_gemm_reduce": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "sca_gemm_tile_override": ([c_int, c_int], c_int),
     "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
     "sca_attn_bwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),

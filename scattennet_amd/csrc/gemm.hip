@@ -843,8 +843,10 @@ extern "C" int sca_gemm_tile_override(int layout, int tile) {
 
 extern "C" void sca_set_error(const char* msg);
 
-extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
-                        void* stream) {
+namespace {
+// do_main: the GEMM launch; do_reduce: the split-K slab reduction (splitk > 1 only)
+int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace, void* stream,
+              bool do_main, bool do_reduce) {
   if (nprob <= 0) return SCA_OK;
   if (nprob > SCA_GEMM_MAX_PROBLEMS || layout < 0 || layout > 2 || splitk < 1) {
     sca_set_error("sca_gemm: bad nprob/layout/splitk");
@@ -896,17 +898,34 @@ extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, in
   long tiles64 = 0;
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
   const int tile = pick_tile(layout, tiles64, splitk);
-  switch (layout) {
+  if (do_main) switch (layout) {
     case SCA_GEMM_NT: rc = launch_tile<SCA_GEMM_NT>(tile, a, nprob, maxM, maxN, st); break;
     case SCA_GEMM_NN: rc = launch_tile<SCA_GEMM_NN>(tile, a, nprob, maxM, maxN, st); break;
     default: rc = launch_tile<SCA_GEMM_TN>(tile, a, nprob, maxM, maxN, st); break;
   }
+  else rc = SCA_OK;
   if (rc != SCA_OK) { sca_set_error("sca_gemm: launch failed"); return rc; }
-  if (splitk > 1) {
+  if (splitk > 1 && do_reduce) {
     const long MN = (long)maxM * maxN;
     dim3 grid((unsigned)((MN + maxM + 255) / 256), nprob);
     hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, a, nprob);
     if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm: reduce launch failed"); return SCA_ERR_LAUNCH; }
   }
   return SCA_OK;
+}
+}  // namespace
+
+extern "C" int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                        void* stream) {
+  return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, true);
+}
+
+extern "C" int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                                void* stream) {
+  return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, false);
+}
+
+extern "C" int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                               void* stream) {
+  return gemm_impl(layout, nprob, probs, splitk, workspace, stream, false, true);
 }

@@ -120,14 +120,36 @@ def sca_grouped(scas, xs, ys, attention_mask):
     causal_mask = key_padding_mask(attention_mask, causal=True)  # model/utils.py:15-28
     cross_mask = self_mask  # create_attention_mask(tgt_len=T) — same key padding
     L = len(scas[0].self_attn_layers)
+    branch = _branch_stream(se[0].device) if (L > 0 and _BRANCH_OVERLAP and se[0].is_cuda) else None
     s = se
-    for i in range(L):
-        s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, self_mask)
+    if branch is not None:
+        # The self stack reads only the x stream and the first causal layer only the y stream:
+        # the self stack runs on a second stream while causal layer 0 runs on this one (host
+        # order, and so dropout-seed order, stays the reference's; each backward node follows
+        # its forward's stream).
+        main = torch.cuda.current_stream(se[0].device)
+        branch.wait_stream(main)
+        for t in list(se) + [self_mask.key_valid]:
+            t.record_stream(branch)
+        with torch.cuda.stream(branch):
+            for i in range(L):
+                s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, self_mask)
+    else:
+        for i in range(L):
+            s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, self_mask)
     c = ce
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
+        if i == 0 and branch is not None:
+            main.wait_stream(branch)
+            for t in s:
+                t.record_stream(main)
         c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask)
     return c, s
+
+
+_BRANCH_OVERLAP = __import__("os").environ.get("SCA_BRANCH_OVERLAP", "1") != "0"
+_branch_stream = ops.branch_stream
 
 
 # --------------------------------------------------------------------------- A1 + A2 + A11 + A12

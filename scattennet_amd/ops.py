@@ -65,7 +65,8 @@ class _timed:
             _PROFILER.records.append((self.key, self.flops, self.e0, self.e1))
 
 
-_GEMM_NAMES = {0: "gemm_kernel<NT,64,64>", 1: "gemm_kernel<NN,64,64>", 2: "gemm_kernel<TN,64,64>"}
+# rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>)
+_GEMM_NAMES = {0: "gemm_glds_kernel<0, 3>", 1: "gemm_glds_kernel<1, 3>", 2: "gemm_glds_kernel<2, 3>"}
 
 # --------------------------------------------------------------------------- launch helpers
 _NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0)
@@ -167,7 +168,10 @@ def gemm(layout, probs, splitk=1, ws=None):
         arr = (L.GemmProblem * len(chunk))(*chunk)
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
         with _timed(_GEMM_NAMES[layout], flops):
-            L.check(lib.sca_gemm(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm")
+            L.check(lib.sca_gemm_partial(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm")
+        if splitk > 1:  # the fixed-order slab reduction: its own launch (timed apart)
+            with _timed("splitk_reduce_kernel", 0.0):
+                L.check(lib.sca_gemm_reduce(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm_reduce")
 
 
 def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
@@ -213,6 +217,19 @@ def _side_stream(device):
     return st
 
 
+_branch_streams = {}
+
+
+def branch_stream(device):
+    """Second compute stream for independent forward branches (the x-stream self stack,
+    keypoint_module.sca_grouped); autograd runs their backward nodes on it as well."""
+    st = _branch_streams.get(device)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _branch_streams[device] = st
+    return st
+
+
 def _queue_join(main, side):
     key = (main.cuda_stream, side.cuda_stream)
     if _join_pending.get(key):
@@ -237,6 +254,11 @@ def weight_grads(items, M=None):
         return _weight_grads(items)
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
+    br = _branch_streams.get(dev)
+    if br is not None and br.cuda_stream == main.cuda_stream:
+        # already off the critical stream; a join queued into it would land after autograd
+        # joined it back (an unjoined fork under graph capture)
+        return _weight_grads(items)
     side = _side_stream(dev)
     side.wait_stream(main)  # dY and X are ready on the main stream
     for it in items:  # keep their memory from being reused by the main stream too early
