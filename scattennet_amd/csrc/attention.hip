@@ -141,6 +141,22 @@ __device__ __forceinline__ void store_cols(float* img, const f32x4* r) {
   }
 }
 
+// XCD-aware block order (cdna_hip_programming.md T1): the hardware deals workgroups round-robin
+// over the 8 XCDs (private L2 each).  Renumber so that each XCD gets a contiguous range of
+// (problem, clip, head, block) tiles: the blocks of one (clip, head) re-read the same K/V
+// (or Q/dO) slice, and neighbouring heads share 128-B lines, so both now hit one L2.
+struct TileId {
+  int x, y, z;
+};
+__device__ __forceinline__ TileId xcd_tile() {
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  return TileId{(int)(id % gx), (int)((id / gx) % gy), (int)(id / (gx * gy))};
+}
+
 // ------------------------------------------------------------------------------ forward
 template <int HD, bool ADDMASK, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
@@ -151,13 +167,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
   __shared__ __attribute__((aligned(16))) float Vt[2][HD * KB];
   __shared__ __attribute__((aligned(16))) float Ka[2][KB];
 
-  const sca_attn_fwd_problem& P = a.p[blockIdx.z];
-  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const TileId tid = xcd_tile();
+  const sca_attn_fwd_problem& P = a.p[tid.z];
+  const int b = tid.y / a.H, h = tid.y % a.H;
   const int nqb = (a.Tq + QB - 1) / QB;  // causal: block x is paired with block nqb-1-x
-  const int jobs = (CAUSAL && nqb - 1 - (int)blockIdx.x != (int)blockIdx.x) ? 2 : 1;
+  const int jobs = (CAUSAL && nqb - 1 - tid.x != tid.x) ? 2 : 1;
 #pragma unroll 1
   for (int job = 0; job < jobs; ++job) {
-  const int xb = job ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int xb = job ? nqb - 1 - tid.x : tid.x;
   const int q0 = xb * QB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = lane & 15, grp = lane >> 4;
@@ -303,13 +320,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float Kt[2][HD * KB];
   __shared__ __attribute__((aligned(16))) float Ka[2][KB];
 
-  const sca_attn_bwd_problem& P = a.p[blockIdx.z];
-  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const TileId tid = xcd_tile();
+  const sca_attn_bwd_problem& P = a.p[tid.z];
+  const int b = tid.y / a.H, h = tid.y % a.H;
   const int nqb = (a.Tq + QB - 1) / QB;  // causal: block x is paired with block nqb-1-x
-  const int jobs = (CAUSAL && nqb - 1 - (int)blockIdx.x != (int)blockIdx.x) ? 2 : 1;
+  const int jobs = (CAUSAL && nqb - 1 - tid.x != tid.x) ? 2 : 1;
 #pragma unroll 1
   for (int job = 0; job < jobs; ++job) {
-  const int xb = job ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int xb = job ? nqb - 1 - tid.x : tid.x;
   const int q0 = xb * QB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = lane & 15, grp = lane >> 4;
@@ -434,13 +452,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float Dt[2][HD * QB];
   __shared__ __attribute__((aligned(16))) float Sm[2][QB], Sl[2][QB], Sd[2][QB];
 
-  const sca_attn_bwd_problem& P = a.p[blockIdx.z];
-  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+  const TileId tid = xcd_tile();
+  const sca_attn_bwd_problem& P = a.p[tid.z];
+  const int b = tid.y / a.H, h = tid.y % a.H;
   const int nkb = (a.Tk + KB - 1) / KB;  // causal: key block x is paired with block nkb-1-x
-  const int jobs = (CAUSAL && nkb - 1 - (int)blockIdx.x != (int)blockIdx.x) ? 2 : 1;
+  const int jobs = (CAUSAL && nkb - 1 - tid.x != tid.x) ? 2 : 1;
 #pragma unroll 1
   for (int job = 0; job < jobs; ++job) {
-  const int k0 = (job ? nkb - 1 - (int)blockIdx.x : (int)blockIdx.x) * KB;
+  const int k0 = (job ? nkb - 1 - tid.x : tid.x) * KB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kj = lane & 15, grp = lane >> 4;
   const int krow = k0 + 16 * w + kj;
