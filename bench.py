@@ -156,6 +156,15 @@ def main():
                 "step_achieved": round(step_flops / (ms / 1e3) / 1e12, 3),
                 "step_frac": round(step_flops / (ms / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
 
+    # HBM traffic of that kernel: from the committed PMC pass (tools/pmc_traffic.sh: separate
+    # FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic_latest.json")
+    if os.path.exists(tpath):
+        tr = json.load(open(tpath)).get(kname)
+        if tr:
+            roofline["traffic"] = round(tr["bytes_per_launch"])
+            roofline["traffic_source"] = "profiles/traffic_latest.json (rocprofv3 PMC, bytes per launch)"
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not fusion and args.dropout == 0:
         cpu = cpu_baseline(w, model, args.cpu_seconds)
