@@ -428,16 +428,33 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
       total += seg_n[s];
     }
   }
+  // Issue-side state: this lane's DMA source pointers at the first slice of the segment being
+  // issued, and the per-slice step; recomputed only when the issue crosses into the next
+  // segment (slices are issued in order), so a slice costs two pointer adds.
+  int iseg = -1, tseg0 = 0, tend = 0;
+  const float* pa[2] = {nullptr, nullptr};
+  const float* pb[2] = {nullptr, nullptr};
+  long stepA = 0, stepB = 0;
   auto dma = [&](int t, int stage) {
-    int s = 0;
-    while (s + 1 < P.nseg && t >= seg_n[s]) { t -= seg_n[s]; ++s; }
-    const sca_gemm_seg& G = P.seg[s];
-    const int k0 = seg_kbeg[s] + t * GL_BK;
+    while (t >= tend) {
+      ++iseg;
+      tseg0 = tend;
+      tend += seg_n[iseg];
+      const sca_gemm_seg& G = P.seg[iseg];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        pa[c] = gl_src<A_KC>(G.A, G.lda, m0, P.M, seg_kbeg[iseg], c, wave, lane);
+        pb[c] = gl_src<B_KC>(G.B, G.ldb, n0, P.N, seg_kbeg[iseg], c, wave, lane);
+      }
+      stepA = A_KC ? GL_BK : (long)GL_BK * G.lda;
+      stepB = B_KC ? GL_BK : (long)GL_BK * G.ldb;
+    }
+    const long kk = t - tseg0;
     char* base = smem + stage * STAGE;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      gl_dma(gl_src<A_KC>(G.A, G.lda, m0, P.M, k0, c, wave, lane), base + gl_dst<A_KC>(c, wave));
-      gl_dma(gl_src<B_KC>(G.B, G.ldb, n0, P.N, k0, c, wave, lane), base + GL_OP_BYTES + gl_dst<B_KC>(c, wave));
+      gl_dma(pa[c] + kk * stepA, base + gl_dst<A_KC>(c, wave));
+      gl_dma(pb[c] + kk * stepB, base + GL_OP_BYTES + gl_dst<B_KC>(c, wave));
     }
   };
 
