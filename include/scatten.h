@@ -67,7 +67,7 @@ typedef struct {
   const float* A;
   const float* B;
   int lda, ldb;
-  int K;       /* reduction length of this segment (multiple of 4) */
+  int K;       /* reduction length of this segment (multiple of 4 for NT / NN; any for TN) */
   float alpha; /* scales A on load: alpha=0.5 reproduces v_proj(kv/2) exactly */
 } sca_gemm_seg;
 

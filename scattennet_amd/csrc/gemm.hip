@@ -883,9 +883,11 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
     for (int s = 0; s < P.nseg; ++s) {
       const sca_gemm_seg& S = P.seg[s];
       const bool a_kc = layout != SCA_GEMM_TN, b_kc = layout == SCA_GEMM_NT;
-      if ((S.K & 3) || !S.A || !S.B || (S.lda & 3) || (S.ldb & 3) ||
+      // K must be a multiple of 4 when an operand is k-contiguous (float4 loads along k); the
+      // TN layout (weight gradients: K = B*T rows) takes any K
+      if (((a_kc || b_kc) && (S.K & 3)) || !S.A || !S.B || (S.lda & 3) || (S.ldb & 3) ||
           (reinterpret_cast<uintptr_t>(S.A) & 15) || (reinterpret_cast<uintptr_t>(S.B) & 15)) {
-        sca_set_error("sca_gemm: K, lda, ldb must be multiples of 4 and A/B 16-byte aligned");
+        sca_set_error("sca_gemm: K (NT/NN), lda, ldb must be multiples of 4 and A/B 16-byte aligned");
         return SCA_ERR_ARG;
       }
       if ((a_kc && S.lda < S.K) || (!a_kc && S.lda < P.M) || (b_kc && S.ldb < S.K) || (!b_kc && S.ldb < P.N)) {
