@@ -187,11 +187,16 @@ def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
 
 def _splitk_for(M_red, n_out_tiles):
     """Split the long reduction (rows of the batch) of weight-gradient GEMMs so that the
-    grid covers the 256 CUs about twice."""
+    grid covers the 256 CUs about four times (measured best for the concurrent side-stream
+    weight gradients: tools/gemm_bench.py and bench.py sweeps via SCA_SPLITK_TILES)."""
     sk = 1
-    while sk < 8 and n_out_tiles * sk < 512 and M_red // (sk * 2) >= 256:
+    while sk < _SPLITK_MAX and n_out_tiles * sk < _SPLITK_TILES and M_red // (sk * 2) >= 256:
         sk *= 2
     return sk
+
+
+_SPLITK_MAX = int(__import__("os").environ.get("SCA_SPLITK_MAX", "8"))
+_SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
 
 
 # ---- weight-gradient side stream -------------------------------------------------------
