@@ -119,58 +119,71 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const LnFwdArgs a) {
   }
 }
 
-constexpr int LN_BWD_ROWS = 16;  // rows per workgroup (4 per wave)
+constexpr int LN_BWD_ROWS = 8;  // rows per workgroup (2 per wave)
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const LnBwdArgs a) {
   using RM = RowMap<NV>;
   constexpr int V = RM::kVals;
+  constexpr int RW = LN_BWD_ROWS / 4;          // rows per wave
+  constexpr int RED = NV > 0 ? 256 * NV : 1024;  // partial-row width held in LDS
   const sca_ln_bwd_problem& P = a.p[blockIdx.y];
-  __shared__ float red[2][4][1024];
+  __shared__ float red[2][4][RED];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int N = a.N;
   float pg[V], pb[V], gam[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) pg[i] = pb[i] = 0.f;
   load_row<NV>(gam, P.gamma, lane, N);
-  const int rbeg = blockIdx.x * LN_BWD_ROWS + w * (LN_BWD_ROWS / 4);
+  const int rbeg = blockIdx.x * LN_BWD_ROWS + w * RW;
+  // phase 1: every load of the wave's rows in flight at once (the stores of phase 2 could
+  // alias them, so the compiler would not hoist them on its own)
+  float xv[RW][V], dy[RW][V], mean[RW], rstd[RW];
 #pragma unroll
-  for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
-    const int row = rbeg + rr;
-    if (row >= a.rows) break;
-    const float mean = P.mean[row], rstd = P.rstd[row];
-    float xv[V], dy[V], t[V];
-    load_row<NV>(xv, P.x + (long)row * N, lane, N);
+  for (int rr = 0; rr < RW; ++rr) {
+    const int row = min(rbeg + rr, a.rows - 1);
+    mean[rr] = P.mean[row];
+    rstd[rr] = P.rstd[row];
+    load_row<NV>(xv[rr], P.x + (long)row * N, lane, N);
+    load_row<NV>(dy[rr], P.dy + (long)row * N, lane, N);
     if (P.r) {
+      float t[V];
       load_row<NV>(t, P.r + rrow(row, a.r_mod, a.r_off) * N, lane, N);
 #pragma unroll
-      for (int i = 0; i < V; ++i) xv[i] += t[i];
+      for (int i = 0; i < V; ++i) xv[rr][i] += t[i];
     }
-    load_row<NV>(dy, P.dy + (long)row * N, lane, N);
     if (P.act) {
+      float t[V];
       load_row<NV>(t, P.y + (long)row * N, lane, N);
 #pragma unroll
       for (int i = 0; i < V; ++i)
-        if (!(t[i] > 0.f)) dy[i] = 0.f;  // ReLU gate (threshold_backward: out > 0)
+        if (!(t[i] > 0.f)) dy[rr][i] = 0.f;  // ReLU gate (threshold_backward: out > 0)
     }
-    if (P.dpost) store_row<NV>(P.dpost + (long)row * N, dy, lane, N);
+  }
+  // phase 2
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) {
+    const int row = rbeg + rr;
+    if (row >= a.rows) break;
+    if (P.dpost) store_row<NV>(P.dpost + (long)row * N, dy[rr], lane, N);
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const bool in = NV > 0 || RM::col(lane, i) < N;
-      xv[i] = in ? (xv[i] - mean) * rstd : 0.f;  // x-hat
-      const float g = dy[i] * gam[i];
+      xv[rr][i] = in ? (xv[rr][i] - mean[rr]) * rstd[rr] : 0.f;  // x-hat
+      const float g = dy[rr][i] * gam[i];
       sg += g;
-      sgx += g * xv[i];
-      pg[i] += dy[i] * xv[i];
-      pb[i] += dy[i];
+      sgx += g * xv[rr][i];
+      pg[i] += dy[rr][i] * xv[rr][i];
+      pb[i] += dy[rr][i];
     }
     const float mg = wave_sum(sg) / N, mgx = wave_sum(sgx) / N;
     float* dxr = P.dx + (long)row * N;
+    float t[V];
     if (a.accumulate) load_row<NV>(t, dxr, lane, N);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      float d = rstd * (dy[i] * gam[i] - mg - xv[i] * mgx);
+      float d = rstd[rr] * (dy[rr][i] * gam[i] - mg - xv[rr][i] * mgx);
       if (a.accumulate) d += t[i];
       t[i] = d;
     }
@@ -202,31 +215,34 @@ struct ReduceArgs {
   long stride_s, stride_i;
 };
 
-// grid (ceil(N/64), I, nprob), 512 threads: wave w sums s = w, w+8, ...; fixed-order combine.
-__global__ __launch_bounds__(512) void reduce_rows_kernel(const ReduceArgs a) {
+// grid (ceil(N/64), I, nprob), 1024 threads: wave w sums s = w, w+16, ... with 8 loads in
+// flight (the reduction is latency-bound: few workgroups, long strided columns); the 16 wave
+// partials are combined in fixed order (deterministic).
+constexpr int RED_WAVES = 16;
+__global__ __launch_bounds__(1024) void reduce_rows_kernel(const ReduceArgs a) {
   const sca_reduce_problem& P = a.p[blockIdx.z];
-  __shared__ float red[8][64];
+  __shared__ float red[RED_WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
   const int i = blockIdx.y;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.f;
   if (j < a.N) {
     const float* base = P.in + (long)i * a.stride_i + j;
     int s = w;
-    for (; s + 24 < a.S; s += 32) {
-      s0 += base[(long)s * a.stride_s];
-      s1 += base[(long)(s + 8) * a.stride_s];
-      s2 += base[(long)(s + 16) * a.stride_s];
-      s3 += base[(long)(s + 24) * a.stride_s];
+    for (; s + 7 * RED_WAVES < a.S; s += 8 * RED_WAVES) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += base[(long)(s + u * RED_WAVES) * a.stride_s];
     }
-    for (; s < a.S; s += 8) s0 += base[(long)s * a.stride_s];
+    for (; s < a.S; s += RED_WAVES) acc[0] += base[(long)s * a.stride_s];
   }
-  red[w][lane] = (s0 + s1) + (s2 + s3);
+  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (w == 0 && j < a.N) {
     float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t += red[k][lane];
+    for (int k = 0; k < RED_WAVES; ++k) t += red[k][lane];
     t *= P.scale;
     float* o = P.out + (long)i * a.N + j;
     if (a.accumulate) t += *o;
@@ -236,7 +252,7 @@ __global__ __launch_bounds__(512) void reduce_rows_kernel(const ReduceArgs a) {
 
 int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
   dim3 grid((a.N + 63) / 64, a.I, nprob);
-  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(1024), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
