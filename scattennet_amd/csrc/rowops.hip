@@ -437,6 +437,9 @@ __global__ __launch_bounds__(256) void coord_map_fwd_kernel(const MapArgs a) {
 }
 
 // Partial weight gradients: partial[c][chunk][n][k] = sum_{rows in chunk} d{x,y}e[row][n] * {x,y}[row][k]
+// A thread owns one column n: the chunk's 2 x MAP_CHUNK gradient values are loaded into
+// registers up front (one round of loads in flight, not one dependent load per row), then
+// every joint's dot product runs out of registers and the LDS coordinates.
 __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a) {
   const sca_coord_map_bwd_problem& P = a.p[blockIdx.y];
   __shared__ float xs[MAP_CHUNK][MAP_KMAX], ys[MAP_CHUNK][MAP_KMAX];
@@ -445,25 +448,28 @@ __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a
   const int nr = min(MAP_CHUNK, a.rows - row0);
   gather_coords(xs, ys, P.kp, P.idx, K, a.K_all, row0, MAP_CHUNK, a.rows);
   __syncthreads();
-  constexpr int KC = 16;
+  constexpr int KC = 8;
   for (int n = threadIdx.x; n < a.N; n += 256) {
+    float dx[MAP_CHUNK], dy[MAP_CHUNK];
+#pragma unroll
+    for (int r = 0; r < MAP_CHUNK; ++r) {
+      const long off = (long)(row0 + min(r, nr - 1)) * a.N + n;
+      dx[r] = r < nr ? P.dxe[off] : 0.f;
+      dy[r] = r < nr ? P.dye[off] : 0.f;
+    }
+    float* px = P.partial + ((long)blockIdx.x * a.N + n) * K;
+    float* py = P.partial + ((long)(a.nchunk + blockIdx.x) * a.N + n) * K;
     for (int kc = 0; kc < K; kc += KC) {
       float gx[KC], gy[KC];
 #pragma unroll
       for (int j = 0; j < KC; ++j) gx[j] = gy[j] = 0.f;
-      for (int r = 0; r < nr; ++r) {
-        const float dx = P.dxe[(long)(row0 + r) * a.N + n];
-        const float dy = P.dye[(long)(row0 + r) * a.N + n];
 #pragma unroll
-        for (int j = 0; j < KC; ++j) {
-          if (kc + j < K) {
-            gx[j] = fmaf(dx, xs[r][kc + j], gx[j]);
-            gy[j] = fmaf(dy, ys[r][kc + j], gy[j]);
-          }
+      for (int r = 0; r < MAP_CHUNK; ++r)
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {  // rows >= nr carry zero gradients; joints >= K are never stored
+          gx[j] = fmaf(dx[r], xs[r][min(kc + j, MAP_KMAX - 1)], gx[j]);
+          gy[j] = fmaf(dy[r], ys[r][min(kc + j, MAP_KMAX - 1)], gy[j]);
         }
-      }
-      float* px = P.partial + ((long)blockIdx.x * a.N + n) * K;
-      float* py = P.partial + ((long)(a.nchunk + blockIdx.x) * a.N + n) * K;
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
         if (kc + j < K) {
@@ -473,6 +479,23 @@ __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a
       }
     }
   }
+}
+
+// dW{x,y} = fixed-order sum of the chunk partials, every problem (per-problem K) in one launch
+__global__ __launch_bounds__(256) void coord_map_reduce_kernel(const MapBwdArgs a) {
+  const sca_coord_map_bwd_problem& P = a.p[blockIdx.z];
+  const long NK = (long)a.N * P.K;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= NK) return;
+  const float* src = P.partial + (long)blockIdx.y * a.nchunk * NK + e;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int c = 0;
+  for (; c + 3 < a.nchunk; c += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += src[(long)(c + u) * NK];
+  }
+  for (; c < a.nchunk; ++c) acc[0] += src[(long)c * NK];
+  (blockIdx.y ? P.dwy : P.dwx)[e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 // Keypoint gradients (only when the keypoints require grad): one wave per row.
@@ -734,15 +757,12 @@ extern "C" int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* pro
   for (int i = 0; i < nprob; ++i) any_dkp |= probs[i].dkp != nullptr;
   if (any_dkp) hipLaunchKernelGGL(coord_map_bwd_kp_kernel, dim3((rows + 3) / 4, nprob), dim3(256), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_coord_map_bwd: launch failed"); return SCA_ERR_LAUNCH; }
-  // dW = fixed-order sum over row chunks (problems may differ in K: one reduce each)
-  for (int i = 0; i < nprob; ++i) {
-    const int NK = N * probs[i].K;
-    ReduceArgs r;
-    r.p[0] = sca_reduce_problem{probs[i].partial, probs[i].dwx, 1.0f};
-    r.p[1] = sca_reduce_problem{probs[i].partial + (long)a.nchunk * NK, probs[i].dwy, 1.0f};
-    r.S = a.nchunk; r.I = 1; r.N = NK; r.accumulate = 0; r.stride_s = NK; r.stride_i = 0;
-    if (launch_reduce(r, 2, st) != SCA_OK) { sca_set_error("sca_coord_map_bwd: reduce launch failed"); return SCA_ERR_LAUNCH; }
-  }
+  // dW = fixed-order sum over row chunks, all problems in one launch
+  int maxK = 0;
+  for (int i = 0; i < nprob; ++i) maxK = maxK > probs[i].K ? maxK : probs[i].K;
+  hipLaunchKernelGGL(coord_map_reduce_kernel, dim3((unsigned)(((long)N * maxK + 255) / 256), 2, nprob), dim3(256), 0,
+                     st, a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_coord_map_bwd: reduce launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
 

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--cases", default="", help="comma-separated substrings selecting cases")
     ap.add_argument("--tiles", default="", help="comma-separated tile ids")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--kscan", action="store_true", help="fixed-cost probe: NT 4x/12x(2048,256,K) over K")
     args = ap.parse_args()
     if args.lib:
         L.LIB_PATH = os.path.abspath(args.lib)
@@ -79,6 +80,9 @@ def main():
         make_case("NT longK 4x(2048,256,4096)", L.GEMM_NT, [(M, d, 4096)] * 4),
         make_case("NT longK 12x(2048,256,2048)", L.GEMM_NT, [(M, d, 2048)] * 12),
     ]
+    if args.kscan:
+        cases = [make_case(f"NT kscan {n}x(2048,256,{k})", L.GEMM_NT, [(M, d, k)] * n)
+                 for n in (4, 12) for k in (32, 64, 128, 256, 512, 1024)]
     if args.cases:
         cases = [c for c in cases if any(k in c["name"] for k in args.cases.split(","))]
     if args.tiles:
