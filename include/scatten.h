@@ -159,6 +159,11 @@ int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B, int H, int
                  int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream);
 int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B, int H, int Tq, int Tk, int hd,
                  int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream);
+/* Backward kernel choice: enable = 1 (default) runs the single-launch fused kernel where it
+ * applies (hd 16, Tq and Tk <= 256, no add_mask): S / P / dP / dS once per score, dK / dV in
+ * registers, dQ from an LDS image of dS; enable = 0 always runs the split dq + dkdv pair.
+ * Both are deterministic and write dq, dk, dv and delta.                               */
+int sca_attn_bwd_fused(int enable);
 
 /* y = act(LayerNorm(x + r) * gamma + beta + post) over rows of width N (eps given).
  * r row index = (row % r_mod) + r_off  (r_mod = rows for an ordinary residual; r_mod = T,

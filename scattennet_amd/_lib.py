@@ -102,6 +102,7 @@ EXPORTS = {
     "sca_gemm_tile_override": ([c_int, c_int], c_int),
     "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
     "sca_attn_bwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
+    "sca_attn_bwd_fused": ([c_int], c_int),
     "sca_layernorm_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p], c_int),
     "sca_layernorm_bwd_blocks": ([c_int], c_int),
     "sca_layernorm_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p], c_int),

@@ -587,6 +587,188 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
   }  // job
 }
 
+// ------------------------------------------------------------------------------ backward: fused
+// One workgroup = one (problem, clip, head) with every key and query of it (Tq, Tk <= 256,
+// hd = 16, key-padding / causal masks): S, P, dP and dS are computed ONCE per score (the
+// split kernels above recompute S and dP in both), dK / dV accumulate in registers, one
+// launch, no atomics.
+//   wave w owns the key tiles g = 4i + w (i < 4; 16 keys each, interleaved so that the
+//   causal triangle gives every wave the same work): K / V rows and the K^T fragments of
+//   them in registers;
+//   per 64-query block (Q, dO, their transposes and the row stats staged in LDS, double-
+//   buffered one block ahead, delta = rowsum(dO * O) computed at staging), for each
+//   (query tile t, own key tile g): S = Q K^T, dP = dO V^T (key on the lane),
+//     P = exp2(S log2e + add - m - ll), dS = P (dP - delta), dV += dO^T P, dK += Q^T dS,
+//     dS transposed through a wave-private LDS tile (padded rows: conflict-free), and
+//     dQ_w += dS K over the wave's own keys;
+//   the four waves' dQ partials are summed in fixed order through LDS (deterministic).
+// ~55 KB of LDS: two workgroups per CU.
+constexpr int FB_TMAX = 256;
+constexpr int FB_TS = 20;  // row stride of the 16x16 dS transposition tile (16 + 4 pad)
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a) {
+  constexpr int HD = 16, NS = 4;
+  __shared__ __attribute__((aligned(16))) float Qs[2][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Ds[2][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Qt[2][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Dt[2][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Sm[2][QB], Sl[2][QB], Sd[2][QB];
+  __shared__ __attribute__((aligned(16))) float dSw[4][16 * FB_TS];
+  __shared__ __attribute__((aligned(16))) float dQr[4][QB * HD];
+
+  const TileId tid = xcd_tile();
+  const sca_attn_bwd_problem& P = a.p[tid.z];
+  const int b = tid.y / a.H, h = tid.y % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kj = lane & 15, grp = lane >> 4;
+  const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
+  const int Tq = a.Tq, Tk = a.Tk;
+
+  // own key tiles: K, V rows (B operands of S = Q K^T, dP = dO V^T) and K^T fragments
+  // (A operand of dQ^T = K^T dS^T: lane (d = kj, grp) holds K[16g + 4grp + r][d])
+  float kreg[4][NS], vreg[4][NS], kadd[4];
+  f32x4 ktf[4];
+  const float* kb = P.k + (long)b * Tk * a.ldk + h * HD;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int g = 4 * i + w;
+    const int key = 16 * g + kj;
+    const int kc = min(key, Tk - 1);
+    const f32x4 kv = ld4(kb + (long)kc * a.ldk + NS * grp);
+    const f32x4 vv = ld4(P.v + ((long)b * Tk + kc) * a.ldv + h * HD + NS * grp);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      kreg[i][j] = kv[j];
+      vreg[i][j] = vv[j];
+      ktf[i][j] = kb[(long)min(16 * g + 4 * grp + j, Tk - 1) * a.ldk + kj];
+    }
+    kadd[i] = key_add(kv_load(P.key_valid, b, key, Tk), false, key, Tk, plus2);
+  }
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nqb = (Tq + QB - 1) / QB;
+  const float* qbase = P.q + (long)b * Tq * a.ldq + h * HD;
+  const float* dbase = P.dout + (long)b * Tq * a.ldo + h * HD;
+  const float* obase = P.o + (long)b * Tq * a.ldo + h * HD;
+  f32x4 rq[1], rd[1];
+  float cm = 0.f, cl = 0.f, cdel = 0.f;
+  int qbn = 0;
+  auto prefetch = [&](int q0) {
+    blk_load<HD>(rq, qbase, a.ldq, q0, Tq);
+    blk_load<HD>(rd, dbase, a.ldo, q0, Tq);
+    f32x4 ro[1];
+    blk_load<HD>(ro, obase, a.ldo, q0, Tq);
+    // delta of row (threadIdx.x >> 2): 4 consecutive lanes hold its 16 dO*O products
+    float dp = rd[0][0] * ro[0][0] + rd[0][1] * ro[0][1] + rd[0][2] * ro[0][2] + rd[0][3] * ro[0][3];
+    dp += __shfl_xor(dp, 1, 64);
+    dp += __shfl_xor(dp, 2, 64);
+    cdel = dp;
+    if (threadIdx.x < QB) {
+      const int q = q0 + threadIdx.x;
+      const long si = ((long)b * a.H + h) * Tq + min(q, Tq - 1);
+      cm = P.stat_m[si];
+      cl = P.stat_ll[si];
+      if (q >= Tq) cm = INFINITY;  // rows past the end: p = exp2(-inf) = 0
+    }
+    qbn = q0;
+  };
+  auto commit = [&](int buf) {
+    store_rows<HD>(Qs[buf], rq);
+    store_cols<HD>(Qt[buf], rq);
+    store_rows<HD>(Ds[buf], rd);
+    store_cols<HD>(Dt[buf], rd);
+    if (threadIdx.x < QB) {
+      Sm[buf][threadIdx.x] = cm;
+      Sl[buf][threadIdx.x] = cl;
+    }
+    if ((threadIdx.x & 3) == 0) {
+      const int row = threadIdx.x >> 2;
+      Sd[buf][row] = cdel;
+      if (qbn + row < Tq) P.delta[((long)b * a.H + h) * Tq + qbn + row] = cdel;
+    }
+  };
+  prefetch(0);
+  commit(0);
+  float* tw = dSw[w];
+
+#pragma unroll 1
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int buf = qb & 1;
+    __syncthreads();  // block qb staged; the previous block's dQ partials consumed
+    if (qb + 1 < nqb) prefetch((qb + 1) * QB);  // in flight during this block
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f32x4 qv = row_frag<HD>(Qs[buf], 16 * t + kj, grp);
+      const f32x4 dov = row_frag<HD>(Ds[buf], 16 * t + kj, grp);
+      const f32x4 dtf = col_frag(Dt[buf], kj, 4 * t + grp);
+      const f32x4 qtf = col_frag(Qt[buf], kj, 4 * t + grp);
+      const int ql = 16 * t + 4 * grp;
+      const f32x4 sm = ld4(&Sm[buf][ql]), sl = ld4(&Sl[buf][ql]), sd = ld4(&Sd[buf][ql]);
+      f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int g = 4 * i + w;
+        if (16 * g >= Tk) continue;                    // wave-uniform: no keys in this tile
+        if (CAUSAL && g > 4 * qb + t) continue;        // every key after every query of the tile
+        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = s_acc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s_acc = mfma16(qv[j], kreg[i][j], s_acc);
+          dp_acc = mfma16(dov[j], vreg[i][j], dp_acc);
+        }
+        float p[4], ds[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t2 = fmaf(s_acc[r], L2E, kadd[i]);
+          if (CAUSAL && g == 4 * qb + t && kj > 4 * grp + r) t2 = -INFINITY;
+          p[r] = fast_exp2((t2 - sm[r]) - sl[r]);
+          ds[r] = p[r] * (dp_acc[r] - sd[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dv[i] = mfma16(dtf[r], p[r], dv[i]);
+          dk[i] = mfma16(qtf[r], ds[r], dk[i]);
+        }
+        // dS^T for dQ: lane (kj, grp) holds dS[q = 4grp + r][key kj]; the B operand wants
+        // lane (q, grp') holding keys 4grp' .. 4grp' + 3 of row q
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tw[(4 * grp + r) * FB_TS + kj] = ds[r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const f32x4 dsv = ld4(&tw[kj * FB_TS + 4 * grp]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dq = mfma16(ktf[i][r], dsv[r], dq);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the tile is rewritten
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      // partial dQ^T[d = 4grp + r][q = 16t + kj] over this wave's keys
+      st4(&dQr[w][(16 * t + kj) * HD + 4 * grp], dq);
+    }
+    __syncthreads();  // all four partials of the block written
+    const int qrow = qb * QB + 16 * w + kj;
+    if (qrow < Tq) {
+      const int e = (16 * w + kj) * HD + 4 * grp;
+      const f32x4 s = ((ld4(&dQr[0][e]) + ld4(&dQr[1][e])) + ld4(&dQr[2][e])) + ld4(&dQr[3][e]);
+      st4(P.dq + ((long)b * Tq + qrow) * a.ldq + h * HD + 4 * grp, s * P.dq_scale);
+    }
+    if (qb + 1 < nqb) commit(buf ^ 1);
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int key = 16 * (4 * i + w) + kj;
+    if (key < Tk) {
+      st4(P.dk + ((long)b * Tk + key) * a.ldk + h * HD + 4 * grp, dk[i]);
+      st4(P.dv + ((long)b * Tk + key) * a.ldv + h * HD + 4 * grp, dv[i] * P.dv_scale);
+    }
+  }
+}
+
 template <typename Args>
 int check_common(const Args& a, int hd, int nprob) {
   if (nprob < 1 || nprob > SCA_ATTN_MAX_PROBLEMS || a.B < 1 || a.H < 1 || a.Tq < 1 || a.Tk < 1) return 1;
@@ -603,8 +785,16 @@ void launch_fwd(const FwdArgs& a, dim3 grid, hipStream_t st) {
   else hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, false>), grid, dim3(256), 0, st, a);
 }
 
+bool g_bwd_fused = true;
+
 template <int HD, bool AM>
 void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st) {
+  if (HD == 16 && !AM && g_bwd_fused && a.Tq <= FB_TMAX && a.Tk <= FB_TMAX) {
+    const dim3 g(1, a.B * a.H, gq.z);
+    if (a.causal) hipLaunchKernelGGL(attn_bwd_fused_kernel<true>, g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(attn_bwd_fused_kernel<false>, g, dim3(256), 0, st, a);
+    return;
+  }
   if (a.causal) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, true>), gq, dim3(256), 0, st, a);
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, true>), gk, dim3(256), 0, st, a);
@@ -617,6 +807,11 @@ void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st) {
 }  // namespace
 
 extern "C" void sca_set_error(const char* msg);
+
+extern "C" int sca_attn_bwd_fused(int enable) {
+  g_bwd_fused = enable != 0;
+  return SCA_OK;
+}
 
 extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B, int H, int Tq, int Tk, int hd,
                             int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream) {

@@ -19,15 +19,34 @@ CASES = [  # kind, B, Tq, Tk, d, H
     ("cross", 3, 70, 45, 64, 4),      # hd 16, Tq != Tk
     ("cross", 2, 33, 129, 128, 4),    # hd 32, Tk > Tq
     ("self", 2, 1, 1, 64, 4),         # single frame
+    # hd 16 with Tq, Tk <= 256: the fused single-launch backward (sca_attn_bwd_fused)
+    ("self", 3, 256, 256, 256, 16),   # the production shape (BASELINE config 2)
+    ("causal", 3, 256, 256, 256, 16),
+    ("cross", 3, 256, 256, 256, 16),
+    ("causal", 3, 130, 130, 64, 4),   # partial last query block and key tile
+    ("self", 3, 200, 200, 32, 2),
+    ("cross", 2, 17, 250, 64, 4),
 ]
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("kind,B,Tq,Tk,d,H", CASES)
-def test_attention_shapes_vs_oracle(kind, B, Tq, Tk, d, H):
+def test_attention_shapes_vs_oracle(kind, B, Tq, Tk, d, H, fused):
     import scattennet_amd as S
+    from scattennet_amd import _lib as L
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
+    if not fused and d // H != 16:
+        pytest.skip("the fused backward only exists for hd 16")
+    L.lib().sca_attn_bwd_fused(fused)
+    try:
+        _run_case(S, kind, B, Tq, Tk, d, H)
+    finally:
+        L.lib().sca_attn_bwd_fused(1)
+
+
+def _run_case(S, kind, B, Tq, Tk, d, H):
     dev = torch.device("cuda:0")
     torch.manual_seed(Tq * 7 + Tk)
     cls = {"self": S.SelfAttention, "causal": S.SelfCausalAttention, "cross": S.CrossAttention}[kind]
