@@ -108,6 +108,25 @@ int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* probs, int s
 int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                     void* stream);
 
+/* NT GEMM + post-LN LayerNorm in one launch (d_model = 256): per problem
+ *   C = resid + dropout((A B^T + bias) * post_scale)      (exactly sca_gemm's NT epilogue)
+ *   y = (C - mean) * rstd * gamma + beta,  rstd = 1 / sqrt(var + eps)   (nn.LayerNorm)
+ * over each full row of C; mean / rstd saved per row (as sca_layernorm_fwd).  Replaces the
+ * out-projection / fc2 GEMM + LayerNorm pairs of keypoint_module.py:63-72, 99-109.
+ * Requires nseg == 1, N == 256, K a positive multiple of 32, 16-byte aligned operands with
+ * leading dimensions multiple of 4 (y has leading dimension 256), epi 0 or DROPOUT only;
+ * else SCA_ERR_ARG (use sca_gemm + sca_layernorm_fwd).                                    */
+typedef struct {
+  const float* gamma; /* [N] */
+  const float* beta;  /* [N] */
+  float* y;           /* [M, N] */
+  float* mean;        /* [M] */
+  float* rstd;        /* [M] */
+} sca_gemm_ln_problem;
+
+int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
+                void* stream);
+
 /* Tuning knob: force the workgroup tile of one layout (0 = built-in heuristic,
  * 1 = 64x64, 2 = 128x64, 3 = 64x128, 4 = 128x128).  Process-global; not thread-safe.   */
 int sca_gemm_tile_override(int layout, int tile);

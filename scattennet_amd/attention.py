@@ -66,12 +66,14 @@ def _resolve_mask(mask, causal):
     raise TypeError(f"unsupported attention_mask type {type(mask)}")
 
 
-def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0):
+def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln=None):
     """Run G attention operators of the same shape in lock-step (one launch per stage).
 
     kind: "self" | "causal" | "cross".  Returns dropout(out_proj(attn), drop_p), plus the
     operator's own query input when `resid` (the post-LN residual of the enclosing block;
-    residual and dropout ride in the out-projection epilogue)."""
+    residual and dropout ride in the out-projection epilogue).  `ln` (G nn.LayerNorms): the
+    enclosing block's LayerNorm applied to that result — fused into the out-projection
+    launch (sca_gemm_ln) when d_model = 256, a separate LayerNorm launch otherwise."""
     G = len(attns)
     a0 = attns[0]
     for a in attns:
@@ -84,8 +86,16 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0):
         params += a.qkv_params()
     ts = list(hidden) + (list(kv) if kind == "cross" else []) + params + \
         [a.out_proj.weight for a in attns] + [a.out_proj.bias for a in attns]
-    return list(ops.AttentionBlock.apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
-                                         bool(resid), float(drop_p), *ts))
+    d = hidden[0].shape[-1]
+    fuse = ln is not None and ops.ln_fusable(d, d)
+    if fuse:
+        ts += [n.weight for n in ln] + [n.bias for n in ln]
+    out = list(ops.AttentionBlock.apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
+                                        bool(resid), float(drop_p), float(ln[0].eps) if fuse else None, *ts))
+    if ln is not None and not fuse:
+        from .layers import layernorm_grouped
+        out = layernorm_grouped(ln, out)
+    return out
 
 
 class SelfAttention(BaseAttention):

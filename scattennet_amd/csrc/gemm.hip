@@ -520,6 +520,141 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
   epilogue_block<1, 1>(P, accs, m0 + wm, n0 + wn, col, rowh, args.drop_off);
 }
 
+// ------------------------------------------------------------------------------ GEMM + LayerNorm
+// NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
+// v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
+// d_model = N = 256 — a workgroup owns 32 FULL rows (32x256 tile), so the row statistics
+// never leave the workgroup and the separate LayerNorm launch (plus its re-read of v)
+// disappears.  Main loop: the LDS-DMA ring of gemm_glds_kernel (3 stages of A [32][32] +
+// B [256][32], XOR-swizzled 128-B rows); wave w computes columns 64w .. 64w+63 (two
+// 32x32 accumulators).  Epilogue: the 32x256 tile goes through LDS, then each wave
+// normalises 8 rows with float4 lanes and wave reductions (two-pass mean / variance as
+// ln_fwd_kernel).  Writes v (the LayerNorm input, kept for its backward), y, mean, rstd.
+constexpr int LG_BM = 32, LG_BN = 256, LG_S = 3;
+constexpr int LG_A_BYTES = LG_BM * GL_BK * 4;      // 4 KiB
+constexpr int LG_B_BYTES = LG_BN * GL_BK * 4;      // 32 KiB
+constexpr int LG_STAGE = LG_A_BYTES + LG_B_BYTES;  // 36 KiB
+constexpr int LG_VS = LG_BN + 8;                   // row stride of the epilogue tile (bank spread)
+
+struct GemmLnArgs {
+  sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
+  sca_gemm_ln_problem ln[SCA_GEMM_MAX_PROBLEMS];
+  float eps;
+  const unsigned long long* drop_off;
+};
+
+// per-lane source of DMA piece `pc` (rows 8pc .. 8pc+7 of a k-contiguous [rows][32] tile)
+__device__ __forceinline__ const float* lg_src(const float* base, int ld, int row0, int nrows, int pc, int lane) {
+  const int r = 8 * pc + (lane >> 3);
+  const int ks = (lane & 7) ^ gl_swz(r);
+  return base + (long)min(row0 + r, nrows - 1) * ld + 4 * ks;
+}
+
+__global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
+  __shared__ __attribute__((aligned(1024))) char smem[LG_S * LG_STAGE];
+  const unsigned gx = gridDim.x;
+  const unsigned nwg = gx * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * blockIdx.z;
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int pid = wgid / gx, bx = wgid % gx;
+  const sca_gemm_problem& P = args.p[pid];
+  const sca_gemm_ln_problem& LN = args.ln[pid];
+  const int m0 = bx * LG_BM;
+  if (m0 >= P.M) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const sca_gemm_seg& G = P.seg[0];
+  const int total = G.K / GL_BK;
+
+  // this lane's DMA sources: A piece `wave`, B pieces 8*wave .. 8*wave+7
+  // (the swizzle of row r is (r >> 1) & 7: pieces 2u and 2u + 1 differ in it, pieces 16 rows
+  // apart do not — one source pointer per parity, stepped by 16 rows)
+  const float* pa = lg_src(G.A, G.lda, m0, P.M, wave, lane);
+  const float* pb[2] = {lg_src(G.B, G.ldb, 0, P.N, 8 * wave, lane), lg_src(G.B, G.ldb, 0, P.N, 8 * wave + 1, lane)};
+  const long pstep = 16L * G.ldb;
+  auto dma = [&](int t, int stage) {
+    char* base = smem + stage * LG_STAGE;
+    const long kk = (long)t * GL_BK;
+    gl_dma(pa + kk, base + wave * GL_PIECE);
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + LG_A_BYTES + (8 * wave + c) * GL_PIECE);
+  };
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < LG_S - 1; ++i)
+    if (i < total) dma(i, i);
+  for (int t = 0; t < total; ++t) {
+    if (t + LG_S - 2 < total) gl_wait_vm<9 * (LG_S - 2)>();
+    else gl_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + LG_S - 1 < total) dma(t + LG_S - 1, (t + LG_S - 1) % LG_S);
+    const char* As = smem + (t % LG_S) * LG_STAGE;
+    const char* Bs = As + LG_A_BYTES;
+    f32x4 fa[4], fb0[4], fb1[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      fa[g] = gl_frag<true>(As, 0, g, lane);
+      fb0[g] = gl_frag<true>(Bs, 64 * wave, g, lane);
+      fb1[g] = gl_frag<true>(Bs, 64 * wave + 32, g, lane);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc0 = mfma32(fa[g][j], fb0[g][j], acc0);
+        acc1 = mfma32(fa[g][j], fb1[g][j], acc1);
+      }
+  }
+
+  // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
+  __syncthreads();
+  float* V = reinterpret_cast<float*>(smem);
+  const float alpha = G.alpha;
+  const int col = lane & 31, rowh = 4 * (lane >> 5);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = (r & 3) + 8 * (r >> 2) + rowh;
+    V[m * LG_VS + 64 * wave + col] = acc0[r] * alpha;
+    V[m * LG_VS + 64 * wave + 32 + col] = acc1[r] * alpha;
+  }
+  __syncthreads();
+
+  const int n = 4 * lane;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
+  const f32x4 gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
+  DropMask dm;
+  const bool drop = (P.epi & SCA_EPI_DROPOUT) != 0;
+  if (drop) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+  const float invN = 1.0f / LG_BN;
+#pragma unroll 2
+  for (int i = 0; i < LG_BM / 4; ++i) {
+    const int lr = (LG_BM / 4) * wave + i, m = m0 + lr;
+    if (m >= P.M) break;
+    f32x4 v = (ld4(&V[lr * LG_VS + n]) + bias4) * P.post_scale;
+    if (drop) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), v[j]);
+    }
+    if (P.resid) v += ld4(P.resid + (long)m * P.ldr + n);
+    st4(P.C + (long)m * P.ldc + n, v);
+    const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * invN;
+    const f32x4 dv = v - mean;
+    const float var = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3])) * invN;
+    const float rstd = 1.0f / sqrtf(var + args.eps);
+    st4(LN.y + (long)m * LG_BN + n, dv * rstd * gam + bet);
+    if (lane == 0) {
+      LN.mean[m] = mean;
+      LN.rstd[m] = rstd;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ persistent
 // One output tile of the persistent kernel: integers only (wave-uniform).  Pointers and
 // leading dimensions are re-read from the kernel arguments (scalar loads) at each fetch,
@@ -947,4 +1082,42 @@ extern "C" int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* p
 extern "C" int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                                void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, false, true);
+}
+
+extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
+                           void* stream) {
+  if (nprob <= 0) return SCA_OK;
+  if (nprob > SCA_GEMM_MAX_PROBLEMS || !probs || !ln || !(eps >= 0.f)) {
+    sca_set_error("sca_gemm_ln: bad nprob / pointers / eps");
+    return SCA_ERR_ARG;
+  }
+  GemmLnArgs a;
+  a.eps = eps;
+  a.drop_off = sca_drop_offset_ptr();
+  int maxM = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const sca_gemm_problem& P = probs[i];
+    const sca_gemm_ln_problem& L = ln[i];
+    const sca_gemm_seg& S = P.seg[0];
+    const bool al16 = !((reinterpret_cast<uintptr_t>(S.A) | reinterpret_cast<uintptr_t>(S.B) |
+                         reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
+                         reinterpret_cast<uintptr_t>(P.bias) | reinterpret_cast<uintptr_t>(L.y) |
+                         reinterpret_cast<uintptr_t>(L.gamma) | reinterpret_cast<uintptr_t>(L.beta)) & 15);
+    if (P.nseg != 1 || P.N != LG_BN || P.M < 0 || S.K < GL_BK || (S.K % GL_BK) || !S.A || !S.B || !P.C ||
+        !L.gamma || !L.beta || !L.y || !L.mean || !L.rstd || !al16 || (S.lda & 3) || (S.ldb & 3) ||
+        S.lda < S.K || S.ldb < S.K || (P.ldc & 3) || P.ldc < LG_BN || (P.resid && ((P.ldr & 3) || P.ldr < LG_BN)) ||
+        (P.epi & ~SCA_EPI_DROPOUT) || ((P.epi & SCA_EPI_DROPOUT) && !(P.drop_p >= 0.f && P.drop_p < 1.f))) {
+      sca_set_error("sca_gemm_ln: needs one segment, N == 256, K a positive multiple of 32, 16-byte aligned "
+                    "operands with leading dimensions multiple of 4, and no epilogue other than dropout");
+      return SCA_ERR_ARG;
+    }
+    a.p[i] = P;
+    a.ln[i] = L;
+    maxM = maxM > P.M ? maxM : P.M;
+  }
+  if (maxM == 0) return SCA_OK;
+  dim3 grid((maxM + LG_BM - 1) / LG_BM, 1, nprob);
+  hipLaunchKernelGGL(gemm_ln_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
 }

@@ -11,7 +11,7 @@ from torch import nn
 from . import ops
 from .attention import CrossAttention, SelfAttention, SelfCausalAttention, attention_grouped
 from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, coordinate_mapping_grouped, drop_p,
-                     ffn_grouped, layernorm_grouped, pos_embed_layernorm_grouped)
+                     ffn_grouped, pos_embed_layernorm_grouped)
 from .residual import ResidualNetwork, residual_network_grouped
 from .utils import key_padding_mask
 
@@ -47,11 +47,10 @@ def coordinate_attention_grouped(blocks, xs, mask):
     """h = LN(x + Attn(x)); self type: h = LN(h + FFN(h))  (keypoint_module.py:61-80).
     The residual adds ride in the out-projection / fc2 epilogues."""
     kind = "self" if blocks[0].attn_type == "self_attn" else "causal"
-    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=True, drop_p=drop_p(blocks))
-    h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
+    h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=True, drop_p=drop_p(blocks),
+                          ln=[b.attn_layer_norm for b in blocks])
     if kind == "self":
-        h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
-        h = layernorm_grouped([b.last_layer_norm for b in blocks], h)
+        h = ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks])
     return h
 
 
@@ -73,10 +72,9 @@ class CoordinatesMerge(nn.Module):
 
 
 def coordinates_merge_grouped(blocks, ys, xs, mask):
-    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True, drop_p=drop_p(blocks))
-    h = layernorm_grouped([b.attn_layer_norm for b in blocks], h)
-    h = ffn_grouped([b.mlp for b in blocks], h, residual=True)
-    return layernorm_grouped([b.last_layer_norm for b in blocks], h)
+    h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True, drop_p=drop_p(blocks),
+                          ln=[b.attn_layer_norm for b in blocks])
+    return ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks])
 
 
 # --------------------------------------------------------------------------- A11

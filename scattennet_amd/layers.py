@@ -47,13 +47,20 @@ def drop_p(mods, attr="dropout"):
     return p
 
 
-def ffn_grouped(ffns, xs, residual=True):
+def ffn_grouped(ffns, xs, residual=True, ln=None):
     """G-way FFN (layers.py:104-108); with `residual` the enclosing block's residual add is
-    fused (y = FFN(x) + x, keypoint_module.py:71-72 / :108-109)."""
+    fused (y = FFN(x) + x, keypoint_module.py:71-72 / :108-109); `ln` (G nn.LayerNorms): the
+    block's last LayerNorm, fused into the fc2 launch when d_model = 256."""
     G = len(xs)
-    return list(ops.FeedForwardResidual.apply(G, residual, drop_p(ffns), *xs, *[f.fc1.weight for f in ffns],
-                                              *[f.fc1.bias for f in ffns], *[f.fc2.weight for f in ffns],
-                                              *[f.fc2.bias for f in ffns]))
+    ts = [*xs, *[f.fc1.weight for f in ffns], *[f.fc1.bias for f in ffns], *[f.fc2.weight for f in ffns],
+          *[f.fc2.bias for f in ffns]]
+    fuse = ln is not None and ops.ln_fusable(xs[0].shape[-1], ffns[0].fc2.weight.shape[1])
+    if fuse:
+        ts += [n.weight for n in ln] + [n.bias for n in ln]
+    out = list(ops.FeedForwardResidual.apply(G, residual, drop_p(ffns), float(ln[0].eps) if fuse else None, *ts))
+    if ln is not None and not fuse:
+        out = layernorm_grouped(ln, out)
+    return out
 
 
 class FeedForward(nn.Module):

@@ -174,6 +174,56 @@ def gemm(layout, probs, splitk=1, ws=None):
                 L.check(lib.sca_gemm_reduce(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm_reduce")
 
 
+# GEMM + post-LN LayerNorm in one launch (sca_gemm_ln) where the shape allows it
+_FUSE_LN = __import__("os").environ.get("SCA_FUSE_LN", "1") != "0"
+
+
+def ln_fusable(N, K):
+    return _FUSE_LN and N == 256 and K >= 32 and K % 32 == 0
+
+
+def gemm_ln(probs, lns, eps):
+    """probs: NT sca_gemm problems (C receives the LayerNorm input v); lns: GemmLnProblem."""
+    lib = L.lib()
+    st = L.stream_handle()
+    for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
+        chunk, lchunk = probs[i:i + L.GEMM_MAX_PROBLEMS], lns[i:i + L.GEMM_MAX_PROBLEMS]
+        arr = (L.GemmProblem * len(chunk))(*chunk)
+        larr = (L.GemmLnProblem * len(lchunk))(*lchunk)
+        flops = sum(2.0 * p.M * p.N * p.seg[0].K for p in chunk) if _PROFILER else 0.0
+        with _timed("gemm_ln_kernel", flops):
+            L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
+
+
+def _ln_fwd_outputs(xs):
+    """(v, y, mean, rstd) buffers of a fused GEMM + LayerNorm over the rows of xs."""
+    rows = xs[0].numel() // xs[0].shape[-1]
+    return ([torch.empty_like(x) for x in xs], [torch.empty_like(x) for x in xs],
+            [xs[0].new_empty(rows) for _ in xs], [xs[0].new_empty(rows) for _ in xs])
+
+
+def _ln_bwd(dys, x, gam, means, rstds):
+    """Plain LayerNorm backward (no residual table / post / activation): (dx, dgamma, dbeta)."""
+    G = len(x)
+    N = x[0].shape[-1]
+    rows = x[0].numel() // N
+    nblk = L.lib().sca_layernorm_bwd_blocks(rows)
+    dx = [torch.empty_like(t) for t in x]
+    dg = [torch.empty_like(t) for t in gam]
+    db = [torch.empty_like(t) for t in gam]
+    part = [x[0].new_empty(2 * nblk * N) for _ in range(G)]
+    for c in range(0, G, L.LN_MAX_PROBLEMS):
+        gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
+        arr = (L.LnBwdProblem * len(gs))(*[L.LnBwdProblem(dys[g].data_ptr(), x[g].data_ptr(), None,
+                                                            gam[g].data_ptr(), means[g].data_ptr(),
+                                                            rstds[g].data_ptr(), None, 0, None, dx[g].data_ptr(),
+                                                            dg[g].data_ptr(), db[g].data_ptr(), part[g].data_ptr())
+                                             for g in gs])
+        L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, rows, 0, 0, L.stream_handle()),
+                "sca_layernorm_bwd")
+    return dx, dg, db
+
+
 def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
     """pairs: list of (in_tensor, out_tensor_or_view, scale)."""
     lib = L.lib()
@@ -387,8 +437,11 @@ class AttentionBlock(Function):
     into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, *ts):
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, *ts):
         cross = kind == "cross"
+        ln = ln_eps is not None  # post-LN LayerNorm fused into the out-projection (sca_gemm_ln)
+        if ln:
+            gam, bet, ts = ts[-2 * G:-G], ts[-G:], ts[:-2 * G]
         causal = kind == "causal"
         xq = _contig(ts[:G])
         o_ = G
@@ -412,16 +465,25 @@ class AttentionBlock(Function):
             probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
         gemm(L.GEMM_NT, probs)
         o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v)
-        ys = [torch.empty_like(x) for x in xq]
-        # y = x + dropout(o Wo^T + bo)  (keypoint_module.py:63-65 / :99-101) in one epilogue
+        # v = x + dropout(o Wo^T + bo)  (keypoint_module.py:63-65 / :99-101) in one epilogue,
+        # and with `ln` the block's LayerNorm y = LN(v) in the same launch
         seeds = dropout_seeds(G) if drop_p > 0 else [None] * G
-        gemm(L.GEMM_NT, [_prob([_seg(_flat(o[g]), Wo[g], d, d, d)], ys[g], B * T, d, d, bias=bo[g],
-                               resid=_flat(xq[g]) if has_resid else None, ldr=d,
-                               drop=(seeds[g], drop_p) if drop_p > 0 else None) for g in range(G)])
+        if ln:
+            vs, ys, means, rstds = _ln_fwd_outputs(xq)
+        else:
+            ys = vs = [torch.empty_like(x) for x in xq]
+        probs = [_prob([_seg(_flat(o[g]), Wo[g], d, d, d)], vs[g], B * T, d, d, bias=bo[g],
+                       resid=_flat(xq[g]) if has_resid else None, ldr=d,
+                       drop=(seeds[g], drop_p) if drop_p > 0 else None) for g in range(G)]
+        if ln:
+            gemm_ln(probs, [L.GemmLnProblem(gam[g].data_ptr(), bet[g].data_ptr(), ys[g].data_ptr(),
+                                            means[g].data_ptr(), rstds[g].data_ptr()) for g in range(G)], ln_eps)
+        else:
+            gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
-        ctx.drop_p, ctx.seeds = drop_p, seeds
+        ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
-                              *sm, *sl)
+                              *sm, *sl, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
 
     @staticmethod
@@ -444,6 +506,12 @@ class AttentionBlock(Function):
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
         dys = _contig(_zeros_for_none(dys, xq))
+        dgam = dbet = ()
+        if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
+            i += 6 * G
+            vs, gam, means, rstds = (sv[i + j * G:i + (j + 1) * G] for j in range(4))
+            dys, dgam, dbet = _ln_bwd(dys, vs, gam, means, rstds)
+            dgam, dbet = tuple(dgam), tuple(dbet)
         dyo = dys  # gradient of the out-projection output: the dropout mask applied to dY
         if ctx.drop_p > 0:
             dyo = [torch.empty_like(t) for t in dys]
@@ -487,7 +555,8 @@ class AttentionBlock(Function):
                 dW += list(wg[4 * g + j])
             dWo.append(wg[4 * g + 3][0])
             dbo.append(wg[4 * g + 3][1])
-        return (None,) * 9 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + tuple(dbo)
+        return (None,) * 10 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
+            tuple(dbo) + dgam + dbet
 
 
 # --------------------------------------------------------------------------- Linear (+ residual)
@@ -541,9 +610,12 @@ class FeedForwardResidual(Function):
     backward's dX GEMM of fc2 applies GELU' in its epilogue."""
 
     @staticmethod
-    def forward(ctx, G, has_r, drop_p, *ts):
+    def forward(ctx, G, has_r, drop_p, ln_eps, *ts):
         x = _contig(ts[:G])
         W1, b1, W2, b2 = ts[G:2 * G], ts[2 * G:3 * G], ts[3 * G:4 * G], ts[4 * G:5 * G]
+        ln = ln_eps is not None  # the block's last LayerNorm fused into fc2 (sca_gemm_ln)
+        if ln:
+            gam, bet = ts[5 * G:6 * G], ts[6 * G:7 * G]
         L.require_device(*x)
         B, T, d = x[0].shape
         M = B * T
@@ -556,12 +628,20 @@ class FeedForwardResidual(Function):
         gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
                                epi=L.EPI_GELU, aux_out=zs[g], ldo=F_,
                                drop=(s1[g], drop_p) if drop_p > 0 else None) for g in range(G)])
-        ys = [torch.empty_like(x[g]) for g in range(G)]
-        gemm(L.GEMM_NT, [_prob([_seg(acts[g], W2[g], F_, F_, F_)], ys[g], M, d, d, bias=b2[g],
-                               resid=_flat(x[g]) if has_r else None, ldr=d,
-                               drop=(s2[g], drop_p) if drop_p > 0 else None) for g in range(G)])
-        ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2 = G, has_r, drop_p, s1, s2
-        ctx.save_for_backward(*x, *W1, *W2, *zs, *acts)
+        if ln:
+            vs, ys, means, rstds = _ln_fwd_outputs(x)
+        else:
+            ys = vs = [torch.empty_like(x[g]) for g in range(G)]
+        probs = [_prob([_seg(acts[g], W2[g], F_, F_, F_)], vs[g], M, d, d, bias=b2[g],
+                       resid=_flat(x[g]) if has_r else None, ldr=d,
+                       drop=(s2[g], drop_p) if drop_p > 0 else None) for g in range(G)]
+        if ln:
+            gemm_ln(probs, [L.GemmLnProblem(gam[g].data_ptr(), bet[g].data_ptr(), ys[g].data_ptr(),
+                                            means[g].data_ptr(), rstds[g].data_ptr()) for g in range(G)], ln_eps)
+        else:
+            gemm(L.GEMM_NT, probs)
+        ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
+        ctx.save_for_backward(*x, *W1, *W2, *zs, *acts, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
 
     @staticmethod
@@ -570,6 +650,11 @@ class FeedForwardResidual(Function):
         sv = ctx.saved_tensors
         x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
         dys = _contig(_zeros_for_none(dys, x))
+        dgam = dbet = ()
+        if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
+            vs, gam, means, rstds = (sv[(5 + i) * G:(6 + i) * G] for i in range(4))
+            dys, dgam, dbet = _ln_bwd(dys, vs, gam, means, rstds)
+            dgam, dbet = tuple(dgam), tuple(dbet)
         B, T, d = x[0].shape
         M = B * T
         F_ = W1[0].shape[0]
@@ -591,8 +676,8 @@ class FeedForwardResidual(Function):
         wg = weight_grads(items)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
-        return (None, None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
-            tuple(w for w, _ in dW2) + tuple(b for _, b in dW2)
+        return (None, None, None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
+            tuple(w for w, _ in dW2) + tuple(b for _, b in dW2) + dgam + dbet
 
 
 # --------------------------------------------------------------------------- LayerNorm

@@ -1,0 +1,112 @@
+"""GPU parity of the fused GEMM + post-LN LayerNorm launch (sca_gemm_ln).
+
+* the C ABI directly against a float64 torch restatement of the same epilogue
+  (v = resid + (A W^T + b) * post_scale, y = LayerNorm(v) * gamma + beta), ragged M;
+* the blocks that use it at d_model = 256 (both CoordinateAttention kinds and
+  CoordinatesMerge, keypoint_module.py:61-80, 97-115) against the CPU oracle, with the fused
+  path on and off, forward and every gradient within the north-star 1e-3.
+"""
+import pytest
+import torch
+
+from oracle import sca_oracle as O
+from tests.golden_util import close, rel_err
+
+PARITY_TOL = 1e-3
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+@pytest.mark.parametrize("M,K", [(8192, 256), (2048, 768), (100, 64), (33, 32)])
+def test_gemm_ln_c_abi_vs_float64(M, K):
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    torch.manual_seed(M + K)
+    N = 256
+    A, W = torch.randn(M, K, device=dev), torch.randn(N, K, device=dev) / K ** 0.5
+    bias, resid = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
+    gam, bet = torch.randn(N, device=dev), torch.randn(N, device=dev)
+    v, y = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    prob = ops._prob([ops._seg(A, W, K, K, K)], v, M, N, N, bias=bias, post_scale=0.75, resid=resid, ldr=N)
+    ops.gemm_ln([prob], [L.GemmLnProblem(gam.data_ptr(), bet.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                         rstd.data_ptr())], 1e-5)
+    torch.cuda.synchronize()
+    v64 = resid.double().cpu() + (A.double().cpu() @ W.double().cpu().T + bias.double().cpu()) * 0.75
+    y64 = torch.nn.functional.layer_norm(v64, (N,), gam.double().cpu(), bet.double().cpu(), 1e-5)
+    assert rel_err(v.cpu(), v64) < 1e-5
+    assert rel_err(y.cpu(), y64) < 1e-4
+    assert rel_err(mean.cpu(), v64.mean(-1)) < 1e-4
+    assert rel_err(rstd.cpu(), 1.0 / (v64.var(-1, unbiased=False) + 1e-5).sqrt()) < 1e-4
+
+
+def test_gemm_ln_rejects_other_widths():
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    A, W = torch.randn(64, 64, device=dev), torch.randn(128, 64, device=dev)
+    v = torch.empty(64, 128, device=dev)
+    g = torch.ones(128, device=dev)
+    prob = ops._prob([ops._seg(A, W, 64, 64, 64)], v, 64, 128, 128)
+    with pytest.raises(ValueError):
+        ops.gemm_ln([prob], [L.GemmLnProblem(g.data_ptr(), g.data_ptr(), v.data_ptr(), g.data_ptr(),
+                                             g.data_ptr())], 1e-5)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("block", ["self", "causal", "merge"])
+def test_blocks_d256_vs_oracle(block, fused):
+    _need_gpu()
+    import scattennet_amd as S
+    from scattennet_amd import ops
+    from scattennet_amd.workloads import model_cfg
+    dev = torch.device("cuda:0")
+    torch.manual_seed(11)
+    B, T, d, H = 3, 72, 256, 16
+    cfg = model_cfg(d, H, 1)
+    m = S.CoordinatesMerge(cfg) if block == "merge" else \
+        S.CoordinateAttention(cfg, "self_attn" if block == "self" else "causal_attn")
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn_like(p) / (p.shape[-1] ** 0.5 if p.dim() == 2 else 4.0))
+    m = m.to(dev)
+    x, kv = torch.randn(B, T, d), torch.randn(B, T, d)
+    mask = torch.ones(B, T, dtype=torch.long)
+    mask[1, 40:] = 0
+    mask[2, :] = 0
+    causal = block == "causal"
+    am = S.key_padding_mask(mask.to(dev), causal=causal)
+    xg, kvg = x.to(dev).requires_grad_(True), kv.to(dev).requires_grad_(True)
+    old = ops._FUSE_LN
+    ops._FUSE_LN = fused
+    try:
+        out = m(xg, kvg, am) if block == "merge" else m(xg, am)
+        gout = torch.randn(out.shape)
+        out.backward(gout.to(dev))
+        torch.cuda.synchronize()
+    finally:
+        ops._FUSE_LN = old
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    xr, kvr = x.clone().requires_grad_(True), kv.clone().requires_grad_(True)
+    pp = {"b." + k: v for k, v in p.items()}
+    if block == "merge":
+        ref = O.coordinates_merge(pp, "b", xr, kvr, O.additive_key_mask(mask, tgt_len=T), H)
+    else:
+        amr = O.additive_causal_mask(mask) if causal else O.additive_key_mask(mask, tgt_len=T)
+        ref = O.coordinate_attention(pp, "b", xr, amr, H, "causal_attn" if causal else "self_attn")
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * gout).sum().backward()
+    assert rel_err(xg.grad, xr.grad) < PARITY_TOL
+    if block == "merge":
+        assert rel_err(kvg.grad, kvr.grad) < PARITY_TOL
+    gscale = max(float(v.grad.abs().max()) for v in p.values() if v.grad is not None)
+    named = dict(m.named_parameters())
+    for k, v in p.items():
+        if v.grad is not None:
+            assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))
