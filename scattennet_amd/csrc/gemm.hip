@@ -624,6 +624,9 @@ __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
   }
   __syncthreads();
 
+  // each wave normalises 8 rows at once: every row is 64 lanes x float4 (coalesced), and the
+  // eight rows' reductions are interleaved (independent shuffle chains, one latency each)
+  constexpr int RPW = LG_BM / 4;
   const int n = 4 * lane;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
@@ -632,25 +635,45 @@ __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
   const bool drop = (P.epi & SCA_EPI_DROPOUT) != 0;
   if (drop) dm.init(P.drop_seed, P.drop_p, args.drop_off);
   const float invN = 1.0f / LG_BN;
-#pragma unroll 2
-  for (int i = 0; i < LG_BM / 4; ++i) {
-    const int lr = (LG_BM / 4) * wave + i, m = m0 + lr;
-    if (m >= P.M) break;
-    f32x4 v = (ld4(&V[lr * LG_VS + n]) + bias4) * P.post_scale;
+  f32x4 v[RPW];
+  float s[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int lr = RPW * wave + i, m = min(m0 + lr, P.M - 1);
+    v[i] = (ld4(&V[lr * LG_VS + n]) + bias4) * P.post_scale;
     if (drop) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), v[j]);
+      for (int j = 0; j < 4; ++j) v[i][j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), v[i][j]);
     }
-    if (P.resid) v += ld4(P.resid + (long)m * P.ldr + n);
-    st4(P.C + (long)m * P.ldc + n, v);
-    const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * invN;
-    const f32x4 dv = v - mean;
-    const float var = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3])) * invN;
-    const float rstd = 1.0f / sqrtf(var + args.eps);
-    st4(LN.y + (long)m * LG_BN + n, dv * rstd * gam + bet);
-    if (lane == 0) {
-      LN.mean[m] = mean;
-      LN.rstd[m] = rstd;
+    if (P.resid) v[i] += ld4(P.resid + (long)m * P.ldr + n);
+    s[i] = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) s[i] += __shfl_xor(s[i], o, 64);
+  float q[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const f32x4 dv = v[i] - s[i] * invN;
+    q[i] = (dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) q[i] += __shfl_xor(q[i], o, 64);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = m0 + RPW * wave + i;
+    if (m < P.M) {
+      const float mean = s[i] * invN;
+      const float rstd = 1.0f / sqrtf(q[i] * invN + args.eps);
+      st4(P.C + (long)m * P.ldc + n, v[i]);
+      st4(LN.y + (long)m * LG_BN + n, (v[i] - mean) * rstd * gam + bet);
+      if (lane == 0) {
+        LN.mean[m] = mean;
+        LN.rstd[m] = rstd;
+      }
     }
   }
 }
