@@ -73,6 +73,7 @@ def main():
         make_case("NN dffn2 4x(2048,256,768)", L.GEMM_NN, [(M, d, F)] * 4),
         make_case("TN dW 12x(256,256,2048) sk4", L.GEMM_TN, [(d, d, M)] * 12, splitk=4),
         make_case("TN dW 12x(256,256,2048) sk2", L.GEMM_TN, [(d, d, M)] * 12, splitk=2),
+        make_case("NT as-dW 12x(256,256,2048) sk4", L.GEMM_NT, [(d, d, M)] * 12, splitk=4),
         make_case("TN dW 12x(256,256,2048) sk1", L.GEMM_TN, [(d, d, M)] * 12, splitk=1),
         make_case("TN dW2 4x(256,768,2048) sk4", L.GEMM_TN, [(d, F, M)] * 4, splitk=4),
         make_case("TN dW2 4x(256,768,2048) sk2", L.GEMM_TN, [(d, F, M)] * 4, splitk=2),
