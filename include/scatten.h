@@ -41,7 +41,7 @@ extern "C" {
 #define SCA_ERR_ARG 1      /* invalid shape / alignment / argument */
 #define SCA_ERR_LAUNCH 2   /* hipLaunchKernel failed */
 
-#define SCA_GEMM_MAX_PROBLEMS 12
+#define SCA_GEMM_MAX_PROBLEMS 16
 #define SCA_GEMM_MAX_SEGS 3
 
 /* GEMM layouts: C[M,N] = sum_seg alpha_s * op(A_s) op(B_s)                           */

@@ -17,7 +17,7 @@ c_u64 = ctypes.c_uint64
 
 GEMM_NT, GEMM_NN, GEMM_TN = 0, 1, 2
 EPI_GELU, EPI_DGELU, EPI_ACCUM, EPI_DROPOUT = 1, 2, 4, 8
-GEMM_MAX_PROBLEMS = 12
+GEMM_MAX_PROBLEMS = 16
 ATTN_MAX_PROBLEMS = 8
 LN_MAX_PROBLEMS = 8
 REDUCE_MAX_PROBLEMS = 16
