@@ -112,10 +112,17 @@ def sca_grouped(scas, xs, ys, attention_mask):
         raise AttributeError("'NoneType' object has no attribute 'size'")  # reference: mask.size()
     x_self = scas[0].x_self
     se, ce = (xs, ys) if x_self else (ys, xs)
-    se = pos_embed_layernorm_grouped([m.self_pos_embed for m in scas], [m.first_self_norm for m in scas], se, p)
-    ce = pos_embed_layernorm_grouped([m.causal_pos_embed for m in scas], [m.first_causal_norm for m in scas], ce, p)
+    tabs = [m.self_pos_embed for m in scas] + [m.causal_pos_embed for m in scas]
+    norms = [m.first_self_norm for m in scas] + [m.first_causal_norm for m in scas]
+    G = len(scas)
+    if p == 0:  # both streams' embedding LayerNorms in one launch
+        both = pos_embed_layernorm_grouped(tabs, norms, list(se) + list(ce), p)
+        se, ce = both[:G], both[G:]
+    else:  # one call (one seed draw) per stream kind, in the reference's order
+        se = pos_embed_layernorm_grouped(tabs[:G], norms[:G], se, p)
+        ce = pos_embed_layernorm_grouped(tabs[G:], norms[G:], ce, p)
     self_mask = key_padding_mask(attention_mask)  # model/utils.py:3-12
-    causal_mask = key_padding_mask(attention_mask, causal=True)  # model/utils.py:15-28
+    causal_mask = self_mask.causal_view()  # model/utils.py:15-28 (same key validity, +1 on j <= i)
     cross_mask = self_mask  # create_attention_mask(tgt_len=T) — same key padding
     L = len(scas[0].self_attn_layers)
     branch = _branch_stream(se[0].device) if (L > 0 and _BRANCH_OVERLAP and se[0].is_cuda) else None

@@ -378,6 +378,12 @@ class KeyPaddingMask:
         self.causal_plus_one = causal_plus_one
         self.key_valid = (mask != 0).to(torch.float32).contiguous()
 
+    def causal_view(self):
+        """The causal variant (create_causal_attention_mask) sharing this key-validity vector."""
+        m = KeyPaddingMask.__new__(KeyPaddingMask)
+        m.mask, m.causal_plus_one, m.key_valid = self.mask, True, self.key_valid
+        return m
+
     @property
     def shape(self):
         return self.mask.shape
@@ -761,7 +767,7 @@ class LayerNormAdd(Function):
         dtab = []
         if pos:
             B, T = x[0].shape[0], x[0].shape[1]
-            dtab = [torch.zeros_like(t) for t in tab]
+            dtab = list(torch.zeros((G,) + tuple(tab[0].shape), device=tab[0].device).unbind(0))  # one fill
             # d table[t + 2] = sum_b dv[b, t]
             reduce_rows([(dx[g], dtab[g][2:], 1.0) for g in range(G)], B, T, N, T * N, N)
         return (None,) * 6 + tuple(dx) + tuple(dtab) + (tuple(dpost) if ctx.has_post else ()) + \
