@@ -219,8 +219,9 @@ typedef struct {
   int act;
   float* dpost;  /* or NULL: receives the (gated) gradient of `post` */
   float* dx;     /* gradient of (x + r); ACCUM adds into dx */
-  float* dgamma; /* [N] written */
-  float* dbeta;  /* [N] written */
+  float* dgamma; /* [N] written; NULL: the affine partials stay in `partial` (rows 0..nblk-1
+                  * sum to dgamma, rows nblk..2nblk-1 to dbeta) for a later sca_reduce_rows */
+  float* dbeta;  /* [N] written (ignored when dgamma is NULL) */
   float* partial; /* workspace [2 * nblk * N], nblk from sca_layernorm_bwd_blocks() */
 } sca_ln_bwd_problem;
 

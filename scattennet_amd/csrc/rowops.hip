@@ -690,15 +690,20 @@ extern "C" int sca_layernorm_bwd(int nprob, const sca_ln_bwd_problem* probs, int
     default: hipLaunchKernelGGL(ln_bwd_kernel<0>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
   }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_layernorm_bwd: launch failed"); return SCA_ERR_LAUNCH; }
-  // dgamma / dbeta = fixed-order sums of the per-workgroup partial rows
+  // dgamma / dbeta = fixed-order sums of the per-workgroup partial rows (problems with
+  // dgamma == NULL leave them in `partial` for the caller's own sca_reduce_rows)
   ReduceArgs r;
   int np = 0;
   for (int i = 0; i < nprob; ++i) {
+    if (!probs[i].dgamma) continue;
     r.p[np++] = sca_reduce_problem{probs[i].partial, probs[i].dgamma, 1.0f};
     r.p[np++] = sca_reduce_problem{probs[i].partial + (long)a.nblk * N, probs[i].dbeta, 1.0f};
   }
   r.S = a.nblk; r.I = 1; r.N = N; r.accumulate = 0; r.stride_s = N; r.stride_i = 0;
-  if (launch_reduce(r, np, st) != SCA_OK) { sca_set_error("sca_layernorm_bwd: reduce launch failed"); return SCA_ERR_LAUNCH; }
+  if (np && launch_reduce(r, np, st) != SCA_OK) {
+    sca_set_error("sca_layernorm_bwd: reduce launch failed");
+    return SCA_ERR_LAUNCH;
+  }
   return SCA_OK;
 }
 

@@ -174,6 +174,9 @@ def gemm(layout, probs, splitk=1, ws=None):
                 L.check(lib.sca_gemm_reduce(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm_reduce")
 
 
+# the fused LayerNorms' dgamma / dbeta reductions ride in the weight-gradient side section
+_LN_AFFINE_SIDE = __import__("os").environ.get("SCA_LN_AFFINE_SIDE", "1") != "0"
+
 # GEMM + post-LN LayerNorm in one launch (sca_gemm_ln) where the shape allows it
 _FUSE_LN = __import__("os").environ.get("SCA_FUSE_LN", "1") != "0"
 
@@ -202,8 +205,12 @@ def _ln_fwd_outputs(xs):
             [xs[0].new_empty(rows) for _ in xs], [xs[0].new_empty(rows) for _ in xs])
 
 
-def _ln_bwd(dys, x, gam, means, rstds):
-    """Plain LayerNorm backward (no residual table / post / activation): (dx, dgamma, dbeta)."""
+def _ln_bwd(dys, x, gam, means, rstds, defer_affine=False, params=None):
+    """Plain LayerNorm backward (no residual table / post / activation): (dx, dgamma, dbeta,
+    finish).  With `defer_affine` the dgamma / dbeta reduction is NOT launched here:
+    `finish` = (launch function, its input tensors) is run by the caller later — inside the
+    weight-gradient side-stream section (weight_grads(..., extra=finish)), so that the
+    parameter-only reduction leaves the critical stream without a fork of its own."""
     G = len(x)
     N = x[0].shape[-1]
     rows = x[0].numel() // N
@@ -217,11 +224,17 @@ def _ln_bwd(dys, x, gam, means, rstds):
         arr = (L.LnBwdProblem * len(gs))(*[L.LnBwdProblem(dys[g].data_ptr(), x[g].data_ptr(), None,
                                                             gam[g].data_ptr(), means[g].data_ptr(),
                                                             rstds[g].data_ptr(), None, 0, None, dx[g].data_ptr(),
-                                                            dg[g].data_ptr(), db[g].data_ptr(), part[g].data_ptr())
-                                             for g in gs])
+                                                            None if defer_affine else dg[g].data_ptr(),
+                                                            None if defer_affine else db[g].data_ptr(),
+                                                            part[g].data_ptr()) for g in gs])
         L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, rows, 0, 0, L.stream_handle()),
                 "sca_layernorm_bwd")
-    return dx, dg, db
+    finish = None
+    if defer_affine:
+        finish = (lambda: reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
+                                      [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0),
+                  part, params or ())
+    return dx, dg, db, finish
 
 
 def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
@@ -298,29 +311,40 @@ def _queue_join(main, side):
     torch.autograd.Variable._execution_engine.queue_callback(_join)
 
 
-def weight_grads(items, M=None):
+def weight_grads(items, M=None, extra=None):
     """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
     the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
 
     items: list of (dY[M,out], X[M,in], alpha, W_like, has_bias[, bias_scale]) -> [(dW, db)].
     bias_scale defaults to alpha; it differs when alpha scales the INPUT X (v from kv/2:
     dWv = dV^T (kv/2) but dbv = colsum(dV))."""
-    if not _WGRAD_SIDE:
-        return _weight_grads(items)
+    def run():
+        out = _weight_grads(items)
+        if extra is not None:
+            extra[0]()
+        return out
+
+    # a parameter that already holds a .grad gets the new gradient added by autograd as soon
+    # as this returns (ordered on the current stream only): compute on the current stream
+    params = [it[3] for it in items] + list(extra[2] if extra is not None else ())
+    if not _WGRAD_SIDE or any(p.grad is not None for p in params):
+        return run()
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
     br = _branch_streams.get(dev)
     if br is not None and br.cuda_stream == main.cuda_stream:
         # already off the critical stream; a join queued into it would land after autograd
         # joined it back (an unjoined fork under graph capture)
-        return _weight_grads(items)
+        return run()
     side = _side_stream(dev)
     side.wait_stream(main)  # dY and X are ready on the main stream
     for it in items:  # keep their memory from being reused by the main stream too early
         it[0].record_stream(side)
         it[1].record_stream(side)
+    for t in (extra[1] if extra is not None else ()):
+        t.record_stream(side)
     with torch.cuda.stream(side):
-        out = _weight_grads(items)
+        out = run()
     _queue_join(main, side)
     return out
 
@@ -513,10 +537,12 @@ class AttentionBlock(Function):
         av = 0.5 if cross else 1.0
         dys = _contig(_zeros_for_none(dys, xq))
         dgam = dbet = ()
+        ln_finish = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             i += 6 * G
             vs, gam, means, rstds = (sv[i + j * G:i + (j + 1) * G] for j in range(4))
-            dys, dgam, dbet = _ln_bwd(dys, vs, gam, means, rstds)
+            dys, dgam, dbet, ln_finish = _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE,
+                                                 params=gam)
             dgam, dbet = tuple(dgam), tuple(dbet)
         dyo = dys  # gradient of the out-projection output: the dropout mask applied to dY
         if ctx.drop_p > 0:
@@ -554,7 +580,7 @@ class AttentionBlock(Function):
             items += [(_flat(dq[g]), xf, 1.0, Wq, bq is not None), (_flat(dk[g]), kf, 1.0, Wk, bk is not None),
                       (_flat(dv[g]), kf, 1.0, Wv, bv is not None, 1.0 / av),
                       (_flat(dyo[g]), _flat(o[g]), 1.0, Wo[g], bo[g] is not None)]
-        wg = weight_grads(items)
+        wg = weight_grads(items, extra=ln_finish)
         dW, dWo, dbo = [], [], []
         for g in range(G):
             for j in range(3):
@@ -657,9 +683,11 @@ class FeedForwardResidual(Function):
         x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
         dys = _contig(_zeros_for_none(dys, x))
         dgam = dbet = ()
+        ln_finish = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             vs, gam, means, rstds = (sv[(5 + i) * G:(6 + i) * G] for i in range(4))
-            dys, dgam, dbet = _ln_bwd(dys, vs, gam, means, rstds)
+            dys, dgam, dbet, ln_finish = _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE,
+                                                 params=gam)
             dgam, dbet = tuple(dgam), tuple(dbet)
         B, T, d = x[0].shape
         M = B * T
@@ -679,7 +707,7 @@ class FeedForwardResidual(Function):
                                resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)])
         items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], True) for g in range(G)] + \
                 [(dz[g], _flat(x[g]), 1.0, W1[g], True) for g in range(G)]
-        wg = weight_grads(items)
+        wg = weight_grads(items, extra=ln_finish)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
         return (None, None, None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
