@@ -133,6 +133,7 @@ def sca_grouped(scas, xs, ys, attention_mask):
         # order, and so dropout-seed order, stays the reference's; each backward node follows
         # its forward's stream).
         main = torch.cuda.current_stream(se[0].device)
+        _branch_stream(se[0].device, main)  # records the join target of the branch
         branch.wait_stream(main)
         for t in list(se) + [self_mask.key_valid]:
             t.record_stream(branch)

@@ -273,28 +273,33 @@ _SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
 import os as _os
 
 _WGRAD_SIDE = _os.environ.get("SCA_WGRAD_STREAM", "1") != "0"
+_BRANCH_SIDE = _os.environ.get("SCA_BRANCH_SIDE", "1") != "0"  # branch-stream weight grads on their own side stream
 _side_streams = {}
 _join_pending = {}
 
 
-def _side_stream(device):
-    st = _side_streams.get(device)
+def _side_stream(device, which=0):
+    st = _side_streams.get((device, which))
     if st is None:
         st = torch.cuda.Stream(device=device)
-        _side_streams[device] = st
+        _side_streams[(device, which)] = st
     return st
 
 
 _branch_streams = {}
+_branch_origin = {}  # branch stream ptr -> the stream it was forked from (its join target)
 
 
-def branch_stream(device):
+def branch_stream(device, origin=None):
     """Second compute stream for independent forward branches (the x-stream self stack,
-    keypoint_module.sca_grouped); autograd runs their backward nodes on it as well."""
+    keypoint_module.sca_grouped); autograd runs their backward nodes on it as well.
+    `origin`: the stream the branch forks from and is joined back into."""
     st = _branch_streams.get(device)
     if st is None:
         st = torch.cuda.Stream(device=device)
         _branch_streams[device] = st
+    if origin is not None:
+        _branch_origin[st.cuda_stream] = origin
     return st
 
 
@@ -331,12 +336,19 @@ def weight_grads(items, M=None, extra=None):
         return run()
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
+    join_into = main
     br = _branch_streams.get(dev)
     if br is not None and br.cuda_stream == main.cuda_stream:
-        # already off the critical stream; a join queued into it would land after autograd
-        # joined it back (an unjoined fork under graph capture)
-        return run()
-    side = _side_stream(dev)
+        # on the branch stream (the self stack's backward): fork a second side stream from it,
+        # joined into the stream the branch itself was forked from — the branch has already
+        # been joined back by autograd when the join callback runs (a wait queued into it then
+        # would be an unjoined fork under graph capture)
+        join_into = _branch_origin.get(br.cuda_stream)
+        if join_into is None or not _BRANCH_SIDE:
+            return run()
+        side = _side_stream(dev, 1)
+    else:
+        side = _side_stream(dev)
     side.wait_stream(main)  # dY and X are ready on the main stream
     for it in items:  # keep their memory from being reused by the main stream too early
         it[0].record_stream(side)
@@ -345,7 +357,7 @@ def weight_grads(items, M=None, extra=None):
         t.record_stream(side)
     with torch.cuda.stream(side):
         out = run()
-    _queue_join(main, side)
+    _queue_join(join_into, side)
     return out
 
 
