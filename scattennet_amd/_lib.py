@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libscatten_hip.so")
+LIB_PATH = os.environ.get("SCA_LIB_PATH") or os.path.join(_HERE, "libscatten_hip.so")  # override: A/B builds
 
 c_int, c_float, c_long, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_long, ctypes.c_void_p
 c_u64 = ctypes.c_uint64
