@@ -442,13 +442,19 @@ __global__ __launch_bounds__(256) void coord_map_fwd_kernel(const MapArgs a) {
 // every joint's dot product runs out of registers and the LDS coordinates.
 __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a) {
   const sca_coord_map_bwd_problem& P = a.p[blockIdx.y];
-  __shared__ float xs[MAP_CHUNK][MAP_KMAX], ys[MAP_CHUNK][MAP_KMAX];
+  __shared__ __attribute__((aligned(16))) float xs[MAP_CHUNK][MAP_KMAX], ys[MAP_CHUNK][MAP_KMAX];
   const int row0 = blockIdx.x * MAP_CHUNK;
   const int K = P.K;
   const int nr = min(MAP_CHUNK, a.rows - row0);
   gather_coords(xs, ys, P.kp, P.idx, K, a.K_all, row0, MAP_CHUNK, a.rows);
-  __syncthreads();
   constexpr int KC = 8;
+  const int Kp = (K + KC - 1) / KC * KC;  // joints padded to whole float4 pairs (zeros)
+  for (int e = threadIdx.x; e < MAP_CHUNK * (Kp - K); e += 256) {
+    const int r = e / (Kp - K), k = K + e % (Kp - K);
+    xs[r][k] = 0.f;
+    ys[r][k] = 0.f;
+  }
+  __syncthreads();
   for (int n = threadIdx.x; n < a.N; n += 256) {
     float dx[MAP_CHUNK], dy[MAP_CHUNK];
 #pragma unroll
@@ -463,13 +469,18 @@ __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a
       float gx[KC], gy[KC];
 #pragma unroll
       for (int j = 0; j < KC; ++j) gx[j] = gy[j] = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < MAP_CHUNK; ++r) {  // rows >= nr carry zero gradients; joints >= K are never stored
+        const f32x4 x0 = ld4(&xs[r][kc]), x1 = ld4(&xs[r][kc + 4]);  // broadcast float4 LDS reads
+        const f32x4 y0 = ld4(&ys[r][kc]), y1 = ld4(&ys[r][kc + 4]);
 #pragma unroll
-      for (int r = 0; r < MAP_CHUNK; ++r)
-#pragma unroll
-        for (int j = 0; j < KC; ++j) {  // rows >= nr carry zero gradients; joints >= K are never stored
-          gx[j] = fmaf(dx[r], xs[r][min(kc + j, MAP_KMAX - 1)], gx[j]);
-          gy[j] = fmaf(dy[r], ys[r][min(kc + j, MAP_KMAX - 1)], gy[j]);
+        for (int j = 0; j < 4; ++j) {
+          gx[j] = fmaf(dx[r], x0[j], gx[j]);
+          gx[j + 4] = fmaf(dx[r], x1[j], gx[j + 4]);
+          gy[j] = fmaf(dy[r], y0[j], gy[j]);
+          gy[j + 4] = fmaf(dy[r], y1[j], gy[j + 4]);
         }
+      }
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
         if (kc + j < K) {
