@@ -342,6 +342,16 @@ int sca_coord_map_bwd_chunks(int rows);
 int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* probs, int rows, int K_all, int N,
                       void* stream);
 
+/* Input contract: SLR_Dataset.normalize_keypoints
+ * (dataset.py:134-170) on a zero-padded batch.  kp_in / kp_out: (B, T, K_all, 2) fp32;
+ * frame t of clip b with t < lengths[b] is normalised part by part, in order (part p owns
+ * joints part_idx[part_off[p] .. part_off[p+1])): its bounding box grown by 5 % of the
+ * longer side and squared, clamped to [0, 1], then x, y mapped into it (an axis whose
+ * clamped extent is 0 is left as is).  Frames t >= lengths[b] are written as zeros (the
+ * collator's padding, dataset.py:82-91).  K_all <= 1024; kp_out may alias kp_in.        */
+int sca_normalize_parts(const float* kp_in, float* kp_out, const int* lengths, int B, int T, int K_all,
+                        const int* part_off, const int* part_idx, int nparts, void* stream);
+
 const char* sca_last_error(void);
 int sca_version(void);
 

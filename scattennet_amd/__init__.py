@@ -12,6 +12,7 @@ from .keypoint_module import (CoordinateAttention, CoordinatesMerge, KeypointMod
                               SeparativeCoordinateAttention)
 from .layers import CoordinateMapping, FeedForward, LearningPositionEmbedding  # noqa: F401
 from .residual import ResidualBlock, ResidualNetwork  # noqa: F401
+from .data import JointParts, collate_keypoints, normalize_keypoints  # noqa: F401
 from .utils import KeyPaddingMask, create_attention_mask, create_causal_attention_mask, key_padding_mask  # noqa: F401
 
 __version__ = "0.1.0"

@@ -122,6 +122,8 @@ EXPORTS = {
     "sca_coord_map_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_coord_map_bwd_chunks": ([c_int], c_int),
     "sca_coord_map_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_normalize_parts": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                             c_void_p], c_int),
     "sca_last_error": ([], ctypes.c_char_p),
     "sca_version": ([], c_int),
 }

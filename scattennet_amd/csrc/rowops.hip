@@ -530,6 +530,84 @@ __global__ __launch_bounds__(256) void coord_map_bwd_kp_kernel(const MapBwdArgs 
   }
 }
 
+// ------------------------------------------------------------------------------ input contract
+// SLR_Dataset.normalize_keypoints (dataset.py:134-170) on the padded batch: one wave per
+// frame, the frame's joints staged in LDS, parts processed in order (a later part sees an
+// earlier part's result, exactly as the reference's in-place loop), wave min / max
+// reductions for the box.
+constexpr int NORM_KMAX = 1024;
+
+struct NormArgs {
+  const float* in;
+  float* out;
+  const int* lengths;
+  const int* part_off;
+  const int* part_idx;
+  int B, T, K_all, nparts;
+};
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void normalize_parts_kernel(const NormArgs a) {
+  __shared__ __attribute__((aligned(16))) float fr[4][2 * NORM_KMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long frame = (long)blockIdx.x * 4 + w;
+  if (frame >= (long)a.B * a.T) return;
+  const int b = (int)(frame / a.T), t = (int)(frame % a.T);
+  const int n2 = 2 * a.K_all;
+  const float* src = a.in + frame * n2;
+  float* dst = a.out + frame * n2;
+  if (t >= a.lengths[b]) {  // collator padding
+    for (int e = lane; e < n2; e += 64) dst[e] = 0.f;
+    return;
+  }
+  float* F = fr[w];
+  for (int e = lane; e < n2; e += 64) F[e] = src[e];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int p = 0; p < a.nparts; ++p) {
+    const int j0 = a.part_off[p], j1 = a.part_off[p + 1];
+    float mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+    for (int j = j0 + lane; j < j1; j += 64) {
+      const int k = a.part_idx[j];
+      mnx = fminf(mnx, F[2 * k]);
+      mxx = fmaxf(mxx, F[2 * k]);
+      mny = fminf(mny, F[2 * k + 1]);
+      mxy = fmaxf(mxy, F[2 * k + 1]);
+    }
+    mnx = wave_min(mnx);
+    mny = wave_min(mny);
+    mxx = wave_max(mxx);
+    mxy = wave_max(mxy);
+    const float wd = mxx - mnx, ht = mxy - mny;
+    float dx, dy;
+    if (wd > ht) {
+      dx = 0.05f * wd;
+      dy = dx + (wd - ht) / 2.0f;
+    } else {
+      dy = 0.05f * ht;
+      dx = dy + (ht - wd) / 2.0f;
+    }
+    const float s0 = fmaxf(0.f, fminf(mnx - dx, 1.f)), s1 = fmaxf(0.f, fminf(mny - dy, 1.f));
+    const float e0 = fmaxf(0.f, fminf(mxx + dx, 1.f)), e1 = fmaxf(0.f, fminf(mxy + dy, 1.f));
+    const float ex = e0 - s0, ey = e1 - s1;
+    for (int j = j0 + lane; j < j1; j += 64) {
+      const int k = a.part_idx[j];
+      if (ex != 0.f) F[2 * k] = (F[2 * k] - s0) / ex;
+      if (ey != 0.f) F[2 * k + 1] = (F[2 * k + 1] - s1) / ey;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next part may share joints
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  for (int e = lane; e < n2; e += 64) dst[e] = F[e];
+}
+
 // ------------------------------------------------------------------------------ dropout
 struct DropArgs {
   sca_dropout_problem p[SCA_DROPOUT_MAX_PROBLEMS];
@@ -804,5 +882,21 @@ extern "C" int sca_dropout(int nprob, const sca_dropout_problem* probs, long row
   const int blocks = (int)(want < 2048 ? (want > 0 ? want : 1) : 2048);
   hipLaunchKernelGGL(dropout_kernel, dim3(blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_dropout: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_normalize_parts(const float* kp_in, float* kp_out, const int* lengths, int B, int T, int K_all,
+                                   const int* part_off, const int* part_idx, int nparts, void* stream) {
+  if (B < 0 || T < 0 || K_all < 1 || K_all > NORM_KMAX || nparts < 0 || !kp_in || !kp_out || !lengths ||
+      (nparts > 0 && (!part_off || !part_idx))) {
+    sca_set_error("sca_normalize_parts: bad arguments (K_all must be 1..1024)");
+    return SCA_ERR_ARG;
+  }
+  const long frames = (long)B * T;
+  if (frames == 0) return SCA_OK;
+  NormArgs a{kp_in, kp_out, lengths, part_off, part_idx, B, T, K_all, nparts};
+  hipLaunchKernelGGL(normalize_parts_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_normalize_parts: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
