@@ -251,7 +251,21 @@ def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
 def _splitk_for(M_red, n_out_tiles):
     """Split the long reduction (rows of the batch) of weight-gradient GEMMs so that the
     grid covers the 256 CUs about four times (measured best for the concurrent side-stream
-    weight gradients: tools/gemm_bench.py and bench.py sweeps via SCA_SPLITK_TILES)."""
+    weight gradients: tools/gemm_bench.py and bench.py sweeps via SCA_SPLITK_TILES).
+    Default (SCA_SPLITK_ROUNDS=1): pick the split that fills whole rounds of the LDS-DMA
+    kernel's 3 workgroups per CU (768 slots) best, each split keeping >= 256 rows (+0.8 %)."""
+    if _SPLITK_ROUNDS:
+        best, best_sk = -1.0, 1
+        for sk in range(1, _SPLITK_MAX + 1):
+            if sk > 1 and M_red // sk < 256:
+                break
+            n = n_out_tiles * sk
+            if n < 512 and sk < _SPLITK_MAX and M_red // (sk + 1) >= 256:
+                continue
+            fill = n / (-(-n // 768) * 768)
+            if fill > best + 1e-9:
+                best, best_sk = fill, sk
+        return best_sk
     sk = 1
     while sk < _SPLITK_MAX and n_out_tiles * sk < _SPLITK_TILES and M_red // (sk * 2) >= 256:
         sk *= 2
@@ -260,6 +274,7 @@ def _splitk_for(M_red, n_out_tiles):
 
 _SPLITK_MAX = int(__import__("os").environ.get("SCA_SPLITK_MAX", "8"))
 _SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
+_SPLITK_ROUNDS = __import__("os").environ.get("SCA_SPLITK_ROUNDS", "1") != "0"
 
 
 # ---- weight-gradient side stream -------------------------------------------------------
