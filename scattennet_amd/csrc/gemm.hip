@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Grouped fp32 GEMM on the gfx950 f32-input matrix cores (v_mfma_f32_32x32x2_f32).
 //
 // Replaces every nn.Linear forward / backward on the SCA hot path (see include/scatten.h
@@ -530,11 +531,19 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
 // 32x32 accumulators).  Epilogue: the 32x256 tile goes through LDS, then each wave
 // normalises 8 rows with float4 lanes and wave reductions (two-pass mean / variance as
 // ln_fwd_kernel).  Writes v (the LayerNorm input, kept for its backward), y, mean, rstd.
-constexpr int LG_BM = 32, LG_BN = 256, LG_S = 3;
-constexpr int LG_A_BYTES = LG_BM * GL_BK * 4;      // 4 KiB
-constexpr int LG_B_BYTES = LG_BN * GL_BK * 4;      // 32 KiB
-constexpr int LG_STAGE = LG_A_BYTES + LG_B_BYTES;  // 36 KiB
-constexpr int LG_VS = LG_BN + 8;                   // row stride of the epilogue tile (bank spread)
+constexpr int LG_BN = 256, GL_A32 = 32, GL_A16 = 16;
+constexpr int LG_B_BYTES = LG_BN * GL_BK * 4;  // 32 KiB
+constexpr int LG_VS = LG_BN + 8;               // row stride of the epilogue tile (bank spread)
+
+// tile variants: 32 rows (3-stage ring, 32x32x2 MFMAs, 1 workgroup / CU) or 16 rows
+// (2-stage ring, 16x16x4 MFMAs, 68 KB LDS: 2 workgroups / CU, twice the workgroups)
+template <int BM>
+struct LgCfg {
+  static constexpr int S = BM == 32 ? 3 : 2;
+  static constexpr int A_BYTES = BM * GL_BK * 4;
+  static constexpr int STAGE = A_BYTES + LG_B_BYTES;
+  static constexpr int A_PIECES = BM / 8;  // 1-KiB DMA pieces of the A tile
+};
 
 struct GemmLnArgs {
   sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
@@ -550,8 +559,16 @@ __device__ __forceinline__ const float* lg_src(const float* base, int ld, int ro
   return base + (long)min(row0 + r, nrows - 1) * ld + 4 * ks;
 }
 
+// float4 of the k-contiguous swizzled image: row r, 16-B slot `slot` (4 consecutive k)
+__device__ __forceinline__ f32x4 lg_slot(const char* img, int r, int slot) {
+  return *(const f32x4*)(img + r * 128 + 16 * (slot ^ gl_swz(r)));
+}
+
+template <int BM>
 __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
-  __shared__ __attribute__((aligned(1024))) char smem[LG_S * LG_STAGE];
+  using CF = LgCfg<BM>;
+  constexpr int S = CF::S;
+  __shared__ __attribute__((aligned(1024))) char smem[S * CF::STAGE];
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
   const unsigned orig = blockIdx.x + gx * blockIdx.z;
@@ -560,73 +577,107 @@ __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
   const int pid = wgid / gx, bx = wgid % gx;
   const sca_gemm_problem& P = args.p[pid];
   const sca_gemm_ln_problem& LN = args.ln[pid];
-  const int m0 = bx * LG_BM;
+  const int m0 = bx * BM;
   if (m0 >= P.M) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const sca_gemm_seg& G = P.seg[0];
   const int total = G.K / GL_BK;
 
-  // this lane's DMA sources: A piece `wave`, B pieces 8*wave .. 8*wave+7
-  // (the swizzle of row r is (r >> 1) & 7: pieces 2u and 2u + 1 differ in it, pieces 16 rows
+  // DMA sources: A pieces spread over the first waves, B pieces 8*wave .. 8*wave+7 (the
+  // swizzle of row r is (r >> 1) & 7: pieces 2u and 2u + 1 differ in it, pieces 16 rows
   // apart do not — one source pointer per parity, stepped by 16 rows)
-  const float* pa = lg_src(G.A, G.lda, m0, P.M, wave, lane);
+  const bool has_a = wave < CF::A_PIECES;
+  const float* pa = lg_src(G.A, G.lda, m0, P.M, has_a ? wave : 0, lane);
   const float* pb[2] = {lg_src(G.B, G.ldb, 0, P.N, 8 * wave, lane), lg_src(G.B, G.ldb, 0, P.N, 8 * wave + 1, lane)};
   const long pstep = 16L * G.ldb;
   auto dma = [&](int t, int stage) {
-    char* base = smem + stage * LG_STAGE;
+    char* base = smem + stage * CF::STAGE;
     const long kk = (long)t * GL_BK;
-    gl_dma(pa + kk, base + wave * GL_PIECE);
+    if (has_a) gl_dma(pa + kk, base + wave * GL_PIECE);
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + LG_A_BYTES + (8 * wave + c) * GL_PIECE);
+      gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + CF::A_BYTES + (8 * wave + c) * GL_PIECE);
   };
 
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
-#pragma unroll
-  for (int i = 0; i < LG_S - 1; ++i)
-    if (i < total) dma(i, i);
-  for (int t = 0; t < total; ++t) {
-    if (t + LG_S - 2 < total) gl_wait_vm<9 * (LG_S - 2)>();
-    else gl_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + LG_S - 1 < total) dma(t + LG_S - 1, (t + LG_S - 1) % LG_S);
-    const char* As = smem + (t % LG_S) * LG_STAGE;
-    const char* Bs = As + LG_A_BYTES;
-    f32x4 fa[4], fb0[4], fb1[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      fa[g] = gl_frag<true>(As, 0, g, lane);
-      fb0[g] = gl_frag<true>(Bs, 64 * wave, g, lane);
-      fb1[g] = gl_frag<true>(Bs, 64 * wave + 32, g, lane);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc0 = mfma32(fa[g][j], fb0[g][j], acc0);
-        acc1 = mfma32(fa[g][j], fb1[g][j], acc1);
-      }
-  }
-
-  // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
-  __syncthreads();
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = G.alpha;
-  const int col = lane & 31, rowh = 4 * (lane >> 5);
+  if constexpr (BM == 32) {
+    f32x16 acc0, acc1;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = (r & 3) + 8 * (r >> 2) + rowh;
-    V[m * LG_VS + 64 * wave + col] = acc0[r] * alpha;
-    V[m * LG_VS + 64 * wave + 32 + col] = acc1[r] * alpha;
+    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i)
+      if (i < total) dma(i, i);
+    for (int t = 0; t < total; ++t) {
+      if (t + S - 2 < total) gl_wait_vm<9 * (S - 2)>();
+      else gl_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+      const char* As = smem + (t % S) * CF::STAGE;
+      const char* Bs = As + CF::A_BYTES;
+      f32x4 fa[4], fb0[4], fb1[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        fa[g] = gl_frag<true>(As, 0, g, lane);
+        fb0[g] = gl_frag<true>(Bs, 64 * wave, g, lane);
+        fb1[g] = gl_frag<true>(Bs, 64 * wave + 32, g, lane);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc0 = mfma32(fa[g][j], fb0[g][j], acc0);
+          acc1 = mfma32(fa[g][j], fb1[g][j], acc1);
+        }
+    }
+    // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
+    __syncthreads();
+    const int col = lane & 31, rowh = 4 * (lane >> 5);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = (r & 3) + 8 * (r >> 2) + rowh;
+      V[m * LG_VS + 64 * wave + col] = acc0[r] * alpha;
+      V[m * LG_VS + 64 * wave + 32 + col] = acc1[r] * alpha;
+    }
+  } else {
+    // 16 rows: wave w owns columns 64w .. 64w+63 as four 16x16 accumulators; per 16-k group
+    // c a lane reads 4 consecutive k of its A row and of each B row (one float4 each)
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int li = lane & 15, grp = lane >> 4;
+    if (total > 0) dma(0, 0);
+    for (int t = 0; t < total; ++t) {
+      gl_wait_vm<0>();               // slice t landed for this wave
+      __builtin_amdgcn_s_barrier();  // ... for every wave; slice t-1's stage no longer read
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < total) dma(t + 1, (t + 1) % S);
+      const char* As = smem + (t % S) * CF::STAGE;
+      const char* Bs = As + CF::A_BYTES;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const f32x4 af = lg_slot(As, li, 4 * c + grp);
+        f32x4 bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = lg_slot(Bs, 64 * wave + 16 * j + li, 4 * c + grp);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = mfma16(af[r], bf[j][r], acc[j]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) V[(4 * grp + r) * LG_VS + 64 * wave + 16 * j + li] = acc[j][r] * alpha;
   }
   __syncthreads();
 
-  // each wave normalises 8 rows at once: every row is 64 lanes x float4 (coalesced), and the
-  // eight rows' reductions are interleaved (independent shuffle chains, one latency each)
-  constexpr int RPW = LG_BM / 4;
+  // each wave normalises BM/4 rows at once: every row is 64 lanes x float4 (coalesced), and
+  // the rows' reductions are interleaved (independent shuffle chains, one latency each)
+  constexpr int RPW = BM / 4;
   const int n = 4 * lane;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
@@ -1139,8 +1190,19 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
     maxM = maxM > P.M ? maxM : P.M;
   }
   if (maxM == 0) return SCA_OK;
-  dim3 grid((maxM + LG_BM - 1) / LG_BM, 1, nprob);
-  hipLaunchKernelGGL(gemm_ln_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  // 16-row tiles (2 workgroups / CU) unless the reduction is long and 32-row tiles already
+  // give a workgroup per CU (measured: tools/gemm_ln_bench.py, bench.py A/B)
+  static const int bm_env = getenv("SCA_GEMM_LN_BM") ? atoi(getenv("SCA_GEMM_LN_BM")) : 0;
+  int maxK = 0;
+  for (int i = 0; i < nprob; ++i) maxK = maxK > probs[i].seg[0].K ? maxK : probs[i].seg[0].K;
+  const long wg32 = (long)nprob * ((maxM + 31) / 32);
+  const int bm = bm_env ? bm_env : ((maxK > 512 && wg32 >= 256) ? 32 : 16);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (bm == 16) {
+    hipLaunchKernelGGL(gemm_ln_kernel<GL_A16>, dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(gemm_ln_kernel<GL_A32>, dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
+  }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

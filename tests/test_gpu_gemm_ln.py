@@ -46,6 +46,34 @@ def test_gemm_ln_c_abi_vs_float64(M, K):
     assert rel_err(rstd.cpu(), 1.0 / (v64.var(-1, unbiased=False) + 1e-5).sqrt()) < 1e-4
 
 
+@pytest.mark.parametrize("K", [768, 256])
+def test_gemm_ln_grouped_row_tiles(K):
+    """Four problems of 2048 rows: K = 768 takes the 32-row tile (a workgroup per CU at 32
+    rows), K = 256 the 16-row tile (sca_gemm_ln's heuristic) — both against float64."""
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    torch.manual_seed(K)
+    M, N, G = 2048, 256, 4
+    probs, lns, keep = [], [], []
+    for g in range(G):
+        A, W = torch.randn(M, K, device=dev), torch.randn(N, K, device=dev) / K ** 0.5
+        b, r = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
+        gam, bet = torch.randn(N, device=dev), torch.randn(N, device=dev)
+        v, y = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+        mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        probs.append(ops._prob([ops._seg(A, W, K, K, K)], v, M, N, N, bias=b, resid=r, ldr=N))
+        lns.append(L.GemmLnProblem(gam.data_ptr(), bet.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr()))
+        keep.append((A, W, b, r, gam, bet, v, y, mean, rstd))  # every buffer alive until the launch ran
+    ops.gemm_ln(probs, lns, 1e-5)
+    torch.cuda.synchronize()
+    for A, W, b, r, gam, bet, v, y, _, _ in keep:
+        v64 = r.double().cpu() + A.double().cpu() @ W.double().cpu().T + b.double().cpu()
+        y64 = torch.nn.functional.layer_norm(v64, (N,), gam.double().cpu(), bet.double().cpu(), 1e-5)
+        assert rel_err(v.cpu(), v64) < 1e-5
+        assert rel_err(y.cpu(), y64) < 1e-4
+
+
 def test_gemm_ln_rejects_other_widths():
     _need_gpu()
     from scattennet_amd import _lib as L, ops
