@@ -95,9 +95,9 @@ typedef struct {
 } sca_gemm_problem;
 
 /* Grouped GEMM over `nprob` independent problems (e.g. q/k/v x streams).
- * splitk > 1 (TN layout, single segment only) writes fp32 partial slabs into
- * `workspace` (nprob * splitk * (M * N + M) floats, problems must share M and N) and
- * reduces them in a second launch in fixed order (deterministic).                       */
+ * splitk > 1 (single segment per problem; shapes may differ) writes fp32 partial slabs
+ * into `workspace` (splitk * sum_p (M_p * N_p + M_p) floats) and reduces them in a second
+ * launch in fixed order (deterministic).                                                  */
 int sca_gemm(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
              void* stream);
 /* The two launches of a split-K sca_gemm issued separately (same arguments): the GEMM

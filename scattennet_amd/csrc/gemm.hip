@@ -35,6 +35,8 @@ struct GemmArgs {
   int tile_prefix[SCA_GEMM_MAX_PROBLEMS + 1];  // cumulative output tiles (x splitk) per problem
   int tiles_n[SCA_GEMM_MAX_PROBLEMS];           // column tiles per problem
   const unsigned long long* drop_off;           // dropout step counter (sca_dropout_offset)
+  long slab_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first partial slab in ws
+  long bias_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first bias partial row in ws
 };
 
 // Workgroup tile configuration.
@@ -306,12 +308,12 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
   const int rowh = 4 * (lane >> 5);
   if (do_bias && threadIdx.x < BM && m0 + (int)threadIdx.x < P.M) {
     if (splitk > 1)
-      args.ws[(long)gridDim.z * P.M * P.N + (long)bz * P.M + m0 + threadIdx.x] = bsum;
+      args.ws[args.bias_off[pid] + (long)ks * P.M + m0 + threadIdx.x] = bsum;
     else
       P.bias_grad[m0 + threadIdx.x] = bsum * P.bias_grad_scale;
   }
   if (splitk > 1) {
-    float* slab = args.ws + (long)bz * P.M * P.N;
+    float* slab = args.ws + args.slab_off[pid] + (long)ks * P.M * P.N;
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
   const int rowh = 4 * (lane >> 5);
   if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
     if (splitk > 1)
-      args.ws[(long)gridDim.z * P.M * P.N + (long)bz * P.M + m0 + threadIdx.x] = bsum * alpha;
+      args.ws[args.bias_off[pid] + (long)ks * P.M + m0 + threadIdx.x] = bsum * alpha;
     else
       P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
   }
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
     for (int r = 0; r < 16; ++r) acc[r] *= alpha;
   }
   if (splitk > 1) {
-    float* slab = args.ws + (long)bz * P.M * P.N;
+    float* slab = args.ws + args.slab_off[pid] + (long)ks * P.M * P.N;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + rowh;
@@ -877,14 +879,13 @@ __global__ __launch_bounds__(C::NT) void gemm_persistent_kernel(const GemmArgs a
     if (sl + 1 >= cur.nsl) {  // tile complete: epilogue (the next tile's loads stay in flight)
       if (do_bias && threadIdx.x < BM && cur.m0 + (int)threadIdx.x < P.M) {
         if (args.splitk > 1)
-          args.ws[(long)args.nprob * args.splitk * P.M * P.N + ((long)cur.pid * args.splitk + cur.ks) * P.M +
-                  cur.m0 + threadIdx.x] = bsum;
+          args.ws[args.bias_off[cur.pid] + (long)cur.ks * P.M + cur.m0 + threadIdx.x] = bsum;
         else
           P.bias_grad[cur.m0 + threadIdx.x] = bsum * P.bias_grad_scale;
       }
       bsum = 0.f;
       if (args.splitk > 1) {
-        float* slab = args.ws + ((long)cur.pid * args.splitk + cur.ks) * P.M * P.N;
+        float* slab = args.ws + args.slab_off[cur.pid] + (long)cur.ks * P.M * P.N;
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -925,7 +926,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args,
   if (e >= MN) {
     const long m = e - MN;
     if (P.bias_grad && m < P.M) {
-      const float* bp = args.ws + (long)nprob * args.splitk * MN + (long)blockIdx.y * args.splitk * P.M + m;
+      const float* bp = args.ws + args.bias_off[blockIdx.y] + m;
       float v = 0.f;
       for (int s = 0; s < args.splitk; ++s) v += bp[(long)s * P.M];
       P.bias_grad[m] = v * P.bias_grad_scale;
@@ -933,7 +934,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args,
     return;
   }
   const int m = (int)(e / P.N), n = (int)(e % P.N);
-  const float* slab = args.ws + (long)blockIdx.y * args.splitk * MN + e;
+  const float* slab = args.ws + args.slab_off[blockIdx.y] + e;
   float v = 0.f;
   for (int s = 0; s < args.splitk; ++s) v += slab[s * MN];
   P.C[(long)m * P.ldc + n] = epilogue(P, m, n, v, args.drop_off);
@@ -1111,8 +1112,8 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
       sca_set_error("sca_gemm: drop_p must be in [0, 1)");
       return SCA_ERR_ARG;
     }
-    if (splitk > 1 && (P.nseg != 1 || P.M != probs[0].M || P.N != probs[0].N)) {
-      sca_set_error("sca_gemm: split-K needs one segment and equal M,N");
+    if (splitk > 1 && P.nseg != 1) {
+      sca_set_error("sca_gemm: split-K needs one segment per problem");
       return SCA_ERR_ARG;
     }
     a.p[i] = P;
@@ -1120,6 +1121,17 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
     maxN = maxN > P.N ? maxN : P.N;
   }
   if (splitk > 1 && !workspace) { sca_set_error("sca_gemm: split-K needs workspace"); return SCA_ERR_ARG; }
+  if (splitk > 1) {  // workspace: every problem's splitk slabs, then every problem's bias partials
+    long o = 0;
+    for (int i = 0; i < nprob; ++i) {
+      a.slab_off[i] = o;
+      o += (long)splitk * probs[i].M * probs[i].N;
+    }
+    for (int i = 0; i < nprob; ++i) {
+      a.bias_off[i] = o;
+      o += (long)splitk * probs[i].M;
+    }
+  }
   if (maxM == 0 || maxN == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;

@@ -274,6 +274,7 @@ def _splitk_for(M_red, n_out_tiles):
 
 _SPLITK_MAX = int(__import__("os").environ.get("SCA_SPLITK_MAX", "8"))
 _SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
+_WGRAD_MIX = __import__("os").environ.get("SCA_WGRAD_MIX", "0") != "0"
 _SPLITK_ROUNDS = __import__("os").environ.get("SCA_SPLITK_ROUNDS", "1") != "0"
 
 
@@ -378,28 +379,29 @@ def weight_grads(items, M=None, extra=None):
 
 def _weight_grads(items):
     out = []
-    by_shape = {}  # split-K needs equal problem shapes within a launch
+    by_shape = {}  # problems of one launch (SCA_WGRAD_MIX=1: any shapes, one launch)
     items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
     for idx, (dY, X, alpha, W, has_bias, _) in enumerate(items):
         n_out, n_in = W.shape
         dW = torch.empty_like(W)
         db = torch.empty(n_out, device=W.device, dtype=W.dtype) if has_bias else None
         out.append((dW, db))
-        by_shape.setdefault((n_out, n_in, dY.shape[0]), []).append(idx)
-    for (n_out, n_in, Mr), idxs in by_shape.items():
-        tiles = ((n_out + 63) // 64) * ((n_in + 63) // 64) * len(idxs)
-        sk = _splitk_for(Mr, tiles)
+        key = (n_out, n_in, dY.shape[0]) if not _WGRAD_MIX else dY.shape[0]
+        by_shape.setdefault(key, []).append(idx)
+    for idxs in by_shape.values():
         for c in range(0, len(idxs), L.GEMM_MAX_PROBLEMS):
             sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
-            probs = []
+            tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
+            sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
+            probs, wsz = [], 0
             for i in sub:
                 dY, X, alpha, W, _, bscale = items[i]
+                n_out, n_in = W.shape
+                Mr = dY.shape[0]
                 probs.append(_prob([_seg(dY, X, n_out, n_in, Mr, alpha)], out[i][0], n_out, n_in, n_in,
                                    bias_grad=out[i][1], bias_grad_scale=bscale / alpha))
-            ws = None
-            if sk > 1:
-                ws = torch.empty(len(sub) * sk * (n_out * n_in + n_out), device=items[0][0].device,
-                                 dtype=torch.float32)
+                wsz += sk * (n_out * n_in + n_out)
+            ws = torch.empty(wsz, device=items[0][0].device, dtype=torch.float32) if sk > 1 else None
             gemm(L.GEMM_TN, probs, splitk=sk, ws=ws)
     return out
 

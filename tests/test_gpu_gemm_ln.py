@@ -138,3 +138,30 @@ def test_blocks_d256_vs_oracle(block, fused):
     for k, v in p.items():
         if v.grad is not None:
             assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))
+
+
+@pytest.mark.parametrize("splitk", [1, 3, 4])
+def test_weight_gradient_gemm_mixed_shapes(splitk):
+    """The TN (weight-gradient) split-K GEMM with problems of different shapes in one launch
+    (fc1 768x256 and fc2 256x768 weight gradients, bias colsums fused) vs float64."""
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    torch.manual_seed(splitk)
+    Mr = 2048
+    shapes = [(768, 256), (256, 768), (256, 256), (64, 32)]
+    probs, keep, wsz = [], [], 0
+    for (n_out, n_in) in shapes:
+        dY, X = torch.randn(Mr, n_out, device=dev), torch.randn(Mr, n_in, device=dev)
+        dW, db = torch.empty(n_out, n_in, device=dev), torch.empty(n_out, device=dev)
+        probs.append(ops._prob([ops._seg(dY, X, n_out, n_in, Mr, 0.5)], dW, n_out, n_in, n_in,
+                               bias_grad=db, bias_grad_scale=2.0))
+        keep.append((dY, X, dW, db))
+        wsz += splitk * (n_out * n_in + n_out)
+    ws = torch.empty(wsz, device=dev) if splitk > 1 else None
+    ops.gemm(L.GEMM_TN, probs, splitk=splitk, ws=ws)
+    torch.cuda.synchronize()
+    for dY, X, dW, db in keep:
+        ref = 0.5 * dY.double().cpu().T @ X.double().cpu()
+        assert rel_err(dW.cpu(), ref) < 1e-5
+        assert rel_err(db.cpu(), dY.double().cpu().sum(0)) < 1e-5
