@@ -1,0 +1,92 @@
+"""torch.library registrations (scattennet_amd/library.py): the operators
+torch.ops.scatten.* against the CPU oracle / torch references, forward and autograd, plus a
+CPU-side check that they are registered with fake (meta) implementations."""
+import pytest
+import torch
+
+from oracle import sca_oracle as O
+from tests.golden_util import rel_err
+
+PARITY_TOL = 1e-3
+
+
+def test_ops_registered_with_fake_impls():
+    import scattennet_amd  # noqa: F401
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    with FakeTensorMode():
+        q = torch.empty(2, 8, 32)
+        o, sm, sl = torch.ops.scatten.masked_attention(q, q, q, None, 2)
+        assert o.shape == q.shape and sm.shape == (2 * 2 * 8,)
+        y, m, r = torch.ops.scatten.layer_norm(q, torch.empty(32), torch.empty(32), 1e-5)
+        assert y.shape == q.shape and m.shape == (16,)
+        kp = torch.empty(2, 5, 10, 2)
+        assert torch.ops.scatten.normalize_keypoints(kp, torch.empty(2), torch.empty(3), torch.empty(4)).shape == kp.shape
+
+
+def test_ops_reject_cpu_tensors():
+    import scattennet_amd  # noqa: F401
+    q = torch.randn(2, 8, 32)
+    with pytest.raises(RuntimeError):
+        torch.ops.scatten.masked_attention(q, q, q, None, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_masked_attention_op_vs_torch(causal):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import scattennet_amd  # noqa: F401
+    torch.manual_seed(5)
+    B, T, H, hd = 3, 70, 4, 16
+    d = H * hd
+    q, k, v = (torch.randn(B, T, d) for _ in range(3))
+    mask = torch.ones(B, T, dtype=torch.long)
+    mask[1, 30:] = 0
+    mask[2, :] = 0
+    dev = "cuda"
+    qg, kg, vg = (t.to(dev).requires_grad_(True) for t in (q, k, v))
+    o = torch.ops.scatten.masked_attention(qg, kg, vg, (mask != 0).float().to(dev), H, causal, causal)[0]
+    g = torch.randn(B, T, d)
+    o.backward(g.to(dev))
+    qr, kr, vr = (t.clone().requires_grad_(True) for t in (q, k, v))
+    am = O.additive_causal_mask(mask) if causal else O.additive_key_mask(mask, tgt_len=T)
+
+    def split(t):
+        return t.view(B, T, H, hd).transpose(1, 2)
+    s = split(qr) @ split(kr).transpose(-1, -2)
+    if causal:
+        s = s.masked_fill(~torch.ones(T, T, dtype=torch.bool).tril(), float("-inf"))
+    ref = (torch.softmax(s + am, dim=-1) @ split(vr)).transpose(1, 2).reshape(B, T, d)
+    assert rel_err(o, ref) < PARITY_TOL
+    (ref * g).sum().backward()
+    for got, want in ((qg, qr), (kg, kr), (vg, vr)):
+        assert rel_err(got.grad, want.grad) < PARITY_TOL
+
+
+@pytest.mark.gpu
+def test_layer_norm_and_normalize_ops():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import numpy as np
+    import scattennet_amd  # noqa: F401
+    torch.manual_seed(6)
+    x, w, b = torch.randn(37, 256), torch.randn(256), torch.randn(256)
+    xg, wg, bg = (t.cuda().requires_grad_(True) for t in (x, w, b))
+    y = torch.ops.scatten.layer_norm(xg, wg, bg, 1e-5)[0]
+    g = torch.randn(37, 256)
+    y.backward(g.cuda())
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    ref = torch.nn.functional.layer_norm(xr, (256,), wr, br, 1e-5)
+    (ref * g).sum().backward()
+    assert rel_err(y, ref) < PARITY_TOL
+    for got, want in ((xg, xr), (wg, wr), (bg, br)):
+        assert rel_err(got.grad, want.grad) < PARITY_TOL
+    parts = [list(range(3)), list(range(3, 9))]
+    kp = np.random.default_rng(0).uniform(0, 1, size=(2, 4, 9, 2)).astype(np.float32)
+    off = torch.tensor([0, 3, 9], dtype=torch.int32, device="cuda")
+    idx = torch.arange(9, dtype=torch.int32, device="cuda")
+    got = torch.ops.scatten.normalize_keypoints(torch.from_numpy(kp).cuda(), torch.tensor([4, 2], device="cuda"),
+                                               off, idx)
+    want = np.stack([O.normalize_keypoints(kp[0], parts), np.concatenate([O.normalize_keypoints(kp[1, :2], parts),
+                                                                          np.zeros_like(kp[1, 2:])])])
+    np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-5, atol=1e-6)
