@@ -53,9 +53,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SCA_DIST_BACKEND", "nccl") != "nccl":  # rehearsal: ranks may share a GPU
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("SCA_DIST_BACKEND", "nccl")  # nccl == RCCL; gloo: rehearse N>1 on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     w = W.WORKLOADS[args.workload]
 
