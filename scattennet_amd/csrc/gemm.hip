@@ -1056,7 +1056,10 @@ int pick_tile(int layout, long tiles64, int splitk) {
   if (g_tile_override[layout]) return g_tile_override[layout];
   (void)splitk;
   (void)tiles64;
-  return 20;  // LDS-DMA kernel; launch_tile falls back per layout when a shape is not eligible
+  // LDS-DMA kernel; launch_tile falls back per layout when a shape is not eligible.  The
+  // input- and weight-gradient layouts use the 2-stage ring (32 KB: up to 5 workgroups / CU
+  // beside the concurrent streams' kernels; bench.py A/B +0.9 %), the forward 3 stages.
+  return layout == SCA_GEMM_NT ? 20 : 21;
 }
 
 }  // namespace

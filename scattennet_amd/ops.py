@@ -262,7 +262,7 @@ def _splitk_for(M_red, n_out_tiles):
             n = n_out_tiles * sk
             if n < 512 and sk < _SPLITK_MAX and M_red // (sk + 1) >= 256:
                 continue
-            fill = n / (-(-n // 768) * 768)
+            fill = n / (-(-n // _SPLITK_SLOTS) * _SPLITK_SLOTS)
             if fill > best + 1e-9:
                 best, best_sk = fill, sk
         return best_sk
@@ -276,6 +276,7 @@ _SPLITK_MAX = int(__import__("os").environ.get("SCA_SPLITK_MAX", "8"))
 _SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
 _WGRAD_MIX = __import__("os").environ.get("SCA_WGRAD_MIX", "0") != "0"
 _SPLITK_ROUNDS = __import__("os").environ.get("SCA_SPLITK_ROUNDS", "1") != "0"
+_SPLITK_SLOTS = int(__import__("os").environ.get("SCA_SPLITK_SLOTS", "768"))  # workgroup slots per round
 
 
 # ---- weight-gradient side stream -------------------------------------------------------
