@@ -119,7 +119,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const LnFwdArgs a) {
   }
 }
 
-constexpr int LN_BWD_ROWS = 8;  // rows per workgroup (2 per wave)
+#ifndef SCA_LN_BWD_ROWS
+#define SCA_LN_BWD_ROWS 8
+#endif
+constexpr int LN_BWD_ROWS = SCA_LN_BWD_ROWS;  // rows per workgroup (LN_BWD_ROWS / 4 per wave)
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const LnBwdArgs a) {
