@@ -185,11 +185,12 @@ def test_sca_stack_train_dropout(seedlog):
 
 
 @pytest.mark.gpu
-def test_grouped_streams_train_dropout(seedlog):
+@pytest.mark.parametrize("d,H,L", [(64, 4, 2), (256, 16, 1)])  # d 256: GEMM + LayerNorm launches, fused bwd
+def test_grouped_streams_train_dropout(seedlog, d, H, L):
     """Two streams in one grouped launch: each stream gets its own masks."""
     from scattennet_amd import workloads as W
     dev = _dev()
-    w = dict(W.WORKLOADS["cfg1"], groups=[12, 15], B=2, T=32, d=64, H=4, L=2, maxpos=32)
+    w = dict(W.WORKLOADS["cfg1"], groups=[12, 15], B=2, T=32, d=d, H=H, L=L, maxpos=32)
     import scattennet_amd as S
     model = W.build_streams(w, dev, seed=3, init="random")
     for sub in model.modules():  # the block dropouts (cfg["dropout"]); attention_dropout stays 0
