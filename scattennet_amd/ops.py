@@ -66,7 +66,20 @@ class _timed:
 
 
 # rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>)
-_GEMM_NAMES = {0: "gemm_glds_kernel<0, 3>", 1: "gemm_glds_kernel<1, 3>", 2: "gemm_glds_kernel<2, 3>"}
+def _gemm_names():
+    """Kernel name per layout as rocprofv3 reports it (the LDS-DMA ring depth pick_tile
+    chooses: 3 stages forward, 2 for the gradient layouts; SCA_GEMM_TILES overrides)."""
+    stages = {20: 3, 21: 2, 22: 4}
+    default = {0: 20, 1: 21, 2: 21}
+    env = [t.strip() for t in __import__("os").environ.get("SCA_GEMM_TILES", "").split(",")]
+    names = {}
+    for lay in range(3):
+        t = int(env[lay]) if lay < len(env) and env[lay] not in ("", "0") else default[lay]
+        names[lay] = f"gemm_glds_kernel<{lay}, {stages[t]}>" if t in stages else f"gemm_kernel<{lay}>"
+    return names
+
+
+_GEMM_NAMES = _gemm_names()
 
 # --------------------------------------------------------------------------- launch helpers
 _NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0)
@@ -194,7 +207,11 @@ def gemm_ln(probs, lns, eps):
         arr = (L.GemmProblem * len(chunk))(*chunk)
         larr = (L.GemmLnProblem * len(lchunk))(*lchunk)
         flops = sum(2.0 * p.M * p.N * p.seg[0].K for p in chunk) if _PROFILER else 0.0
-        with _timed("gemm_ln_kernel", flops):
+        # the row-tile variant sca_gemm_ln picks (gemm.hip), for the kernel name rocprofv3 shows
+        bm = int(__import__("os").environ.get("SCA_GEMM_LN_BM", "0")) or (
+            32 if (max(p.seg[0].K for p in chunk) > 512 and
+                   len(chunk) * ((max(p.M for p in chunk) + 31) // 32) >= 256) else 16)
+        with _timed(f"gemm_ln_kernel<{bm}>", flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
