@@ -29,6 +29,12 @@
  *   sca_dropout            F.dropout in training mode (keypoint_module.py:64,100,164-165,
  *                          layers.py:105,107, fusion.py:48,54) with a counter-based mask;
  *                          also fused into the GEMM and LayerNorm epilogues
+ *   sca_ctc_loss_fwd/bwd   MSCA_Net.compute_loss (model/__init__.py:241-290): log_softmax,
+ *                          clamp(-100, 0), nn.CTCLoss(blank=0, reduction='none',
+ *                          zero_infinity=True), finite mean, clamp(0, 100)
+ *   sca_seqkd_fwd/bwd      SeqKD (loss.py:5-21) with the distillation weight and
+ *                          clamp(-100, 100) of model/__init__.py:203-214
+ *   sca_clamp              RecognitionHead logit clamp(+-50) (model/__init__.py:54-58)
  */
 #ifndef SCATTEN_H
 #define SCATTEN_H
@@ -351,6 +357,40 @@ int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* probs, int row
  * collator's padding, dataset.py:82-91).  K_all <= 1024; kp_out may alias kp_in.        */
 int sca_normalize_parts(const float* kp_in, float* kp_out, const int* lengths, int B, int T, int K_all,
                         const int* part_off, const int* part_idx, int nparts, void* stream);
+
+/* ---- recognition-head losses --------------------------------
+ * CTC over batch-major logits (B, T, C) (the reference's permute(1, 0, 2) at
+ * model/__init__.py:245 is a view; no copy), labels (B, S) int32 padded, in_len / tgt_len
+ * (B) int32 device vectors.  Per sample: S_b = max(tgt_len, 1), T_b = max(in_len, 1, S_b)
+ * (model/__init__.py:262-266); the caller validates T_b <= T, S_b <= S and labels in [0, C)
+ * (out-of-range values are clamped in-kernel only to stay in bounds).  nll (B, optional):
+ * per-sample losses after zero_infinity; loss (1): clamp(mean over finite nll, 0, 100), 0
+ * when none is finite.  ws: sca_ctc_workspace_floats(B, T, S) floats, kept between the
+ * forward and the backward (row log-sum-exp, alpha, beta, per-sample gradient scale).
+ * bwd: dlogits = d loss / d logits given dloss (1 float, device).  C <= 8192, S <= 1023. */
+#define SCA_CTC_MAX_C 8192
+#define SCA_CTC_MAX_S 1023
+long sca_ctc_workspace_floats(int B, int T, int S);
+int sca_ctc_loss_fwd(const float* logits, const int* labels, const int* in_len, const int* tgt_len, int B, int T,
+                     int C, int S, float* nll, float* loss, float* ws, void* stream);
+int sca_ctc_loss_bwd(const float* logits, const int* labels, const int* in_len, const int* tgt_len, int B, int T,
+                     int C, int S, const float* dloss, const float* ws, float* dlogits, void* stream);
+
+/* SeqKD over R rows of C logits (student, teacher): columns [start, C) only (use_blank=False
+ * -> start 1), temperature temp:
+ *   loss = clamp(weight * temp^2 * (1/R) * sum_rows KL(softmax(q/temp) || log_softmax(s/temp)),
+ *                lo, hi)
+ * (KLDivLoss 'batchmean' over the .view(-1, C') rows).  ws: sca_seqkd_workspace_floats(R).
+ * bwd writes d loss / d student (dstudent) and/or d loss / d teacher (dteacher; NULL when
+ * the teacher is detached, as the reference does), zeros in columns < start.              */
+long sca_seqkd_workspace_floats(int R);
+int sca_seqkd_fwd(const float* student, const float* teacher, int R, int C, int start, float temp, float weight,
+                  float lo, float hi, float* loss, float* ws, void* stream);
+int sca_seqkd_bwd(const float* student, const float* teacher, int R, int C, int start, float temp,
+                  const float* dloss, const float* ws, float* dstudent, float* dteacher, void* stream);
+
+/* torch.clamp(x, lo, hi) over n elements (dy == NULL), or its backward dx = dy * [lo <= x <= hi] */
+int sca_clamp(const float* x, float* y, const float* dy, float* dx, long n, float lo, float hi, void* stream);
 
 const char* sca_last_error(void);
 int sca_version(void);

@@ -124,6 +124,15 @@ EXPORTS = {
     "sca_coord_map_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_normalize_parts": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                              c_void_p], c_int),
+    "sca_ctc_workspace_floats": ([c_int, c_int, c_int], c_long),
+    "sca_ctc_loss_fwd": ([c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 4, c_int),
+    "sca_ctc_loss_bwd": ([c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 4, c_int),
+    "sca_seqkd_workspace_floats": ([c_int], c_long),
+    "sca_seqkd_fwd": ([c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_void_p,
+                       c_void_p, c_void_p], c_int),
+    "sca_seqkd_bwd": ([c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p], c_int),
+    "sca_clamp": ([c_void_p] * 4 + [c_long, c_float, c_float, c_void_p], c_int),
     "sca_last_error": ([], ctypes.c_char_p),
     "sca_version": ([], c_int),
 }
