@@ -35,6 +35,8 @@
  *   sca_seqkd_fwd/bwd      SeqKD (loss.py:5-21) with the distillation weight and
  *                          clamp(-100, 100) of model/__init__.py:203-214
  *   sca_clamp              RecognitionHead logit clamp(+-50) (model/__init__.py:54-58)
+ *   sca_lstm_cell_fwd/bwd  AlignmentModule's bidirectional nn.LSTM cell
+ *                          (model/alignment_module.py:24-30, :68-69)
  */
 #ifndef SCATTEN_H
 #define SCATTEN_H
@@ -391,6 +393,20 @@ int sca_seqkd_bwd(const float* student, const float* teacher, int R, int C, int 
 
 /* torch.clamp(x, lo, hi) over n elements (dy == NULL), or its backward dx = dy * [lo <= x <= hi] */
 int sca_clamp(const float* x, float* y, const float* dy, float* dx, long n, float lo, float hi, void* stream);
+
+/* One time step of a (bi)directional LSTM cell (AlignmentModule's nn.LSTM,
+ * model/alignment_module.py:24-30), batch-major, both directions per launch (direction 1
+ * walks t = T-1 .. 0); gate order i, f, g, o.  The projections around it are sca_gemm
+ * launches.  D = ndir.  fwd: gates (B, D*4H) pre-activations of this step -> act
+ * (B, T, D*4H), c / y (B, T, D*H), and hp (B, T, D*H) = the hidden state each step reads
+ * (h_{t-1} for direction 0, h_{t+1} for direction 1; zero-filled by the caller).
+ * bwd (step k walks t = T-1-k / t = k): dh (B, D*H) = dY_t + dG_{t'} W_hh (NULL at k = 0,
+ * where dy (B, T, D*H) is read instead), dc (B, D*H) carried in place, dg (B, T, D*4H) the
+ * gate pre-activation gradients.                                                          */
+int sca_lstm_cell_fwd(const float* gates, float* act, float* c, float* y, float* hp, int B, int T, int H, int ndir,
+                      int step, void* stream);
+int sca_lstm_cell_bwd(const float* dh, const float* dy, const float* act, const float* c, float* dc, float* dg,
+                      int B, int T, int H, int ndir, int step, void* stream);
 
 const char* sca_last_error(void);
 int sca_version(void);

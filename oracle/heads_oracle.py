@@ -149,3 +149,42 @@ def seqkd(student, teacher, weight=1.0, temp=1.0, use_blank=False, lo=-np.inf, h
     ds[..., st:] = (k * (np.exp(ls) - p)).reshape(*s.shape[:-1], C - st)
     dq[..., st:] = (k * p * (h - (p * h).sum(-1, keepdims=True))).reshape(*s.shape[:-1], C - st)
     return loss, ds, dq
+
+
+def alignment_module(params, x, num_layers=2, bidirectional=True, G=None):
+    """AlignmentModule forward (model/alignment_module.py:63-69) in eval mode as an explicit
+    plain-torch CPU loop (torch fp32 autograd for the gradients): nn.LSTM's cell
+    (i, f, g, o = chunks of x W_ih^T + b_ih + h W_hh^T + b_hh; c = sig(f) c + sig(i) tanh(g);
+    h = sig(o) tanh(c)), direction 1 over reversed time, layers stacked on the concatenated
+    directions, then the gloss Linear.  x: (T, B, In) sequence-first.  params: the module's
+    state_dict names -> arrays.  Returns out (B, T, cls) and, with G, the gradients of
+    (out * G).sum() w.r.t. x and every parameter."""
+    import torch
+    P = {k: torch.tensor(np.asarray(v), dtype=torch.float32, requires_grad=G is not None) for k, v in params.items()}
+    xt = torch.tensor(np.asarray(x), dtype=torch.float32, requires_grad=G is not None)
+    inp = xt
+    D = 2 if bidirectional else 1
+    for layer in range(num_layers):
+        outs = []
+        for d in range(D):
+            s = f"_l{layer}" + ("_reverse" if d else "")
+            w_ih, w_hh = P["rnn.weight_ih" + s], P["rnn.weight_hh" + s]
+            b = P["rnn.bias_ih" + s] + P["rnn.bias_hh" + s]
+            T, B = inp.shape[:2]
+            H = w_hh.shape[1]
+            h = inp.new_zeros(B, H)
+            c = inp.new_zeros(B, H)
+            hs = [None] * T
+            for t in (range(T - 1, -1, -1) if d else range(T)):
+                z = inp[t] @ w_ih.T + h @ w_hh.T + b
+                i, f, g, o = z.split(H, dim=1)
+                c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+                h = torch.sigmoid(o) * torch.tanh(c)
+                hs[t] = h
+            outs.append(torch.stack(hs))
+        inp = torch.cat(outs, dim=-1)
+    out = inp.permute(1, 0, 2) @ P["gloss_layer.weight"].T + P["gloss_layer.bias"]
+    if G is None:
+        return out.detach().numpy()
+    (out * torch.tensor(np.asarray(G), dtype=torch.float32)).sum().backward()
+    return out.detach().numpy(), xt.grad.numpy(), {k: v.grad.numpy() for k, v in P.items()}

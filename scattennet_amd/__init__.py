@@ -13,6 +13,7 @@ from .keypoint_module import (CoordinateAttention, CoordinatesMerge, KeypointMod
 from .layers import CoordinateMapping, FeedForward, LearningPositionEmbedding  # noqa: F401
 from .residual import ResidualBlock, ResidualNetwork  # noqa: F401
 from .data import JointParts, collate_keypoints, normalize_keypoints  # noqa: F401
+from .alignment import AlignmentModule  # noqa: F401
 from .heads import RecognitionHead, SeqKD, compute_loss, distillation_loss  # noqa: F401
 from . import library  # noqa: F401  (torch.ops.scatten.*)
 from .utils import KeyPaddingMask, create_attention_mask, create_causal_attention_mask, key_padding_mask  # noqa: F401

@@ -133,6 +133,8 @@ EXPORTS = {
     "sca_seqkd_bwd": ([c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p], c_int),
     "sca_clamp": ([c_void_p] * 4 + [c_long, c_float, c_float, c_void_p], c_int),
+    "sca_lstm_cell_fwd": ([c_void_p] * 5 + [c_int] * 5 + [c_void_p], c_int),
+    "sca_lstm_cell_bwd": ([c_void_p] * 6 + [c_int] * 5 + [c_void_p], c_int),
     "sca_last_error": ([], ctypes.c_char_p),
     "sca_version": ([], c_int),
 }

@@ -355,6 +355,73 @@ __global__ __launch_bounds__(256) void clamp_kernel(const float* __restrict__ x,
   }
 }
 
+
+// ------------------------------------------------------------------------------------ LSTM
+// AlignmentModule's bidirectional nn.LSTM (model/alignment_module.py:24-30), batch-major.
+// The input projection, the per-step recurrent product h W_hh^T (+ b_hh + the projection
+// row, as GEMM epilogue) and all weight / input gradients are sca_gemm launches; these
+// two kernels are the pointwise cell of one time step, both directions in one launch
+// (grid.y = direction; direction 1 walks t = T-1 .. 0).  Layouts, D = ndir:
+//   gates (B, D*4H) this step's pre-activations, gate order i, f, g, o (torch's)
+//   act   (B, T, D*4H) saved activations      c, y (B, T, D*H) cell / hidden states
+//   hp    (B, T, D*H) the hidden state each step READS: h_{t-1} (dir 0) / h_{t+1} (dir 1),
+//         zero where there is none (the caller zero-fills it once)
+//   dh, dc (B, D*H) scratch of the backward walk;  dg (B, T, D*4H) gate pre-activation grads
+struct LstmArgs {
+  const float* gates;
+  float *act, *c, *y, *hp;
+  const float *dh, *dy;
+  float *dc, *dg;
+  int B, T, H, D, step;
+};
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(LstmArgs a) {
+  const int dir = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= a.B * a.H) return;
+  const int b = idx / a.H, j = idx - b * a.H, H = a.H, DH = a.D * H;
+  const int t = dir ? a.T - 1 - a.step : a.step;
+  const int tp = dir ? t + 1 : t - 1, tn = dir ? t - 1 : t + 1;
+  const long row = (long)b * a.T + t;
+  const float* g = a.gates + (long)b * 4 * DH + dir * 4 * H;
+  const float gi = sigm(g[j]), gf = sigm(g[H + j]), gg = tanhf(g[2 * H + j]), go = sigm(g[3 * H + j]);
+  const float cp = (tp >= 0 && tp < a.T) ? a.c[((long)b * a.T + tp) * DH + dir * H + j] : 0.0f;
+  const float c = gf * cp + gi * gg;
+  const float h = go * tanhf(c);
+  a.c[row * DH + dir * H + j] = c;
+  a.y[row * DH + dir * H + j] = h;
+  if (tn >= 0 && tn < a.T) a.hp[((long)b * a.T + tn) * DH + dir * H + j] = h;
+  float* ac = a.act + row * 4 * DH + dir * 4 * H;
+  ac[j] = gi; ac[H + j] = gf; ac[2 * H + j] = gg; ac[3 * H + j] = go;
+}
+
+// backward step `step` walks t = T-1-step (dir 0) / t = step (dir 1); dh holds
+// dY_t + dG_{t'} W_hh (GEMM with the dY row as residual) except at step 0, where it is dY_t
+__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(LstmArgs a) {
+  const int dir = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= a.B * a.H) return;
+  const int b = idx / a.H, j = idx - b * a.H, H = a.H, DH = a.D * H;
+  const int t = dir ? a.step : a.T - 1 - a.step;
+  const int tp = dir ? t + 1 : t - 1;
+  const long row = (long)b * a.T + t;
+  const float dh = a.step == 0 ? a.dy[row * DH + dir * H + j] : a.dh[(long)b * DH + dir * H + j];
+  const float dcn = a.step == 0 ? 0.0f : a.dc[(long)b * DH + dir * H + j];
+  const float* ac = a.act + row * 4 * DH + dir * 4 * H;
+  const float gi = ac[j], gf = ac[H + j], gg = ac[2 * H + j], go = ac[3 * H + j];
+  const float tc = tanhf(a.c[row * DH + dir * H + j]);
+  const float cp = (tp >= 0 && tp < a.T) ? a.c[((long)b * a.T + tp) * DH + dir * H + j] : 0.0f;
+  const float dcc = dcn + dh * go * (1.0f - tc * tc);
+  float* dg = a.dg + row * 4 * DH + dir * 4 * H;
+  dg[j] = dcc * gg * gi * (1.0f - gi);
+  dg[H + j] = dcc * cp * gf * (1.0f - gf);
+  dg[2 * H + j] = dcc * gi * (1.0f - gg * gg);
+  dg[3 * H + j] = dh * tc * go * (1.0f - go);
+  a.dc[(long)b * DH + dir * H + j] = dcc * gf;
+}
+
 bool ctc_dims_ok(int B, int T, int C, int S) {
   return B >= 1 && T >= 1 && C >= 1 && C <= SCA_CTC_MAX_C && S >= 1 && S <= SCA_CTC_MAX_S;
 }
@@ -439,5 +506,34 @@ extern "C" int sca_clamp(const float* x, float* y, const float* dy, float* dx, l
   hipLaunchKernelGGL(clamp_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), x, y, dy, dx, n, lo, hi);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_clamp: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_lstm_cell_fwd(const float* gates, float* act, float* c, float* y, float* hp, int B, int T, int H,
+                                 int ndir, int step, void* stream) {
+  if (B < 1 || T < 1 || H < 1 || ndir < 1 || ndir > 2 || step < 0 || step >= T || !gates || !act || !c || !y ||
+      !hp) {
+    sca_set_error("sca_lstm_cell_fwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  LstmArgs a{gates, act, c, y, hp, nullptr, nullptr, nullptr, nullptr, B, T, H, ndir, step};
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((B * H + 255) / 256, ndir), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_lstm_cell_fwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_lstm_cell_bwd(const float* dh, const float* dy, const float* act, const float* c, float* dc,
+                                 float* dg, int B, int T, int H, int ndir, int step, void* stream) {
+  if (B < 1 || T < 1 || H < 1 || ndir < 1 || ndir > 2 || step < 0 || step >= T || !dy || !act || !c || !dc ||
+      !dg || (step > 0 && !dh)) {
+    sca_set_error("sca_lstm_cell_bwd: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  LstmArgs a{nullptr, const_cast<float*>(act), const_cast<float*>(c), nullptr, nullptr, dh, dy, dc, dg,
+             B, T, H, ndir, step};
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((B * H + 255) / 256, ndir), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_lstm_cell_bwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

@@ -2,9 +2,8 @@
 
 * `RecognitionHead` — the four per-stream gloss classifiers of model/__init__.py:10-69
   (`left/right/body_gloss_classifier`, `fuse_coord_classifier`, same state_dict keys), each
-  a `sca_gemm` Linear followed by the HIP clamp(+-50) of :54-58.  The BiLSTM
-  `fuse_alignment_head` (model/alignment_module.py) is not built yet: `forward` returns the
-  other four logits.
+  a `sca_gemm` Linear followed by the HIP clamp(+-50) of :54-58, and the BiLSTM
+  `fuse_alignment_head` (scattennet_amd/alignment.py) when the cfg has `alignment_module`.
 * `compute_loss` — MSCA_Net.compute_loss (model/__init__.py:241-290) as one HIP op chain
   (`sca_ctc_loss_fwd/bwd`): no host syncs — the reference's `.cpu()` of labels / lengths
   and its NaN / inf checks, which each stall the GPU, are gone.  Lengths given as CPU
@@ -20,6 +19,7 @@ from torch.autograd import Function
 
 from . import _lib as L
 from . import ops
+from .alignment import AlignmentModule
 
 
 def _dev_i32(t, device):
@@ -169,7 +169,8 @@ def distillation_loss(student_logits, teacher_logits, weight, T=1.0):
 
 
 class RecognitionHead(nn.Module):
-    """model/__init__.py:10-69 without the BiLSTM alignment head (not native yet)."""
+    """model/__init__.py:10-69 (same state_dict keys); the alignment head is built when
+    cfg["alignment_module"] is present, as the reference's yaml configs always have it."""
 
     def __init__(self, cfg, gloss_tokenizer):
         super().__init__()
@@ -178,6 +179,8 @@ class RecognitionHead(nn.Module):
         self.right_gloss_classifier = nn.Linear(cfg["residual_blocks"][-1], n)
         self.body_gloss_classifier = nn.Linear(cfg["residual_blocks"][-1], n)
         self.fuse_coord_classifier = nn.Linear(cfg["out_fusion_dim"], n)
+        self.fuse_alignment_head = (AlignmentModule(**cfg["alignment_module"], cls_num=n)
+                                    if "alignment_module" in cfg else None)
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 nn.init.xavier_uniform_(m.weight)
@@ -190,4 +193,7 @@ class RecognitionHead(nn.Module):
         zs += list(ops.LinearResidual.apply(1, False, fuse_output, self.fuse_coord_classifier.weight,
                                             self.fuse_coord_classifier.bias))
         left, right, body, fuse = [clamp_logits(z) for z in zs]
-        return {"left": left, "right": right, "body": body, "fuse_coord_gloss_logits": fuse}
+        out = {"left": left, "right": right, "body": body, "fuse_coord_gloss_logits": fuse}
+        if self.fuse_alignment_head is not None:
+            out["alignment_gloss_logits"] = clamp_logits(self.fuse_alignment_head(fuse_output.permute(1, 0, 2)))
+        return out

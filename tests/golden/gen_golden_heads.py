@@ -25,6 +25,7 @@ sys.path.insert(0, REF)
 
 from loss import SeqKD  # noqa: E402
 from model import MSCA_Net  # noqa: E402
+from model.alignment_module import AlignmentModule  # noqa: E402
 
 
 def ctc_case(name, logits, labels, in_len, tgt_len, manifest):
@@ -58,6 +59,25 @@ def kd_case(name, student, teacher, weight, temp, use_blank, detach, manifest):
                         dteacher=(np.zeros_like(teacher) if detach else q.grad.numpy()))
     manifest[name] = {"op": "SeqKD * weight, clamp(-100, 100)", "ref": "loss.py:5-21, model/__init__.py:203-214",
                       "shape": list(student.shape), "loss": float(loss.item())}
+
+
+def align_case(name, B, T, In, Hd, cls, layers, manifest):
+    """AlignmentModule (model/alignment_module.py) in eval mode: sequence-first input, loss
+    (out * G).sum() with G ~ N(0, 1) seeded at 1; gradients w.r.t. input and every parameter."""
+    torch.manual_seed(3)
+    m = AlignmentModule(cls_num=cls, input_size=In, hidden_size=Hd, num_layers=layers, dropout=0.3,
+                        bidirectional=True).eval()
+    x = torch.randn(T, B, In, requires_grad=True)
+    out = m(x)
+    g = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
+    (out * g).sum().backward()
+    arrs = {"x": x.detach().numpy(), "out": out.detach().numpy(), "G": g.numpy(), "dx": x.grad.numpy()}
+    for k, p in m.named_parameters():
+        arrs["param." + k] = p.detach().numpy()
+        arrs["grad." + k] = p.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+    manifest[name] = {"op": "AlignmentModule (eval)", "ref": "model/alignment_module.py:5-69",
+                      "B": B, "T": T, "input_size": In, "hidden_size": Hd, "cls_num": cls, "num_layers": layers}
 
 
 def plant(logits, labels, in_len, tgt_len, boost):
@@ -112,6 +132,8 @@ def main():
     kd_case("heads_kd_distill", st, te, 0.5, 1.0, False, True, fx)
     kd_case("heads_kd_blank_t2", st, te, 1.0, 2.0, True, False, fx)
     kd_case("heads_kd_clamped", st * 40, te, 400.0, 1.0, False, True, fx)
+
+    align_case("heads_align_B3_T12", 3, 12, 64, 64, 20, 2, fx)
 
     with open(os.path.join(HERE, "manifest_heads.json"), "w") as f:
         json.dump(manifest, f, indent=1)

@@ -179,3 +179,61 @@ def test_hip_recognition_head_and_losses_end_to_end():
     dleft = (dctc * gate_l) @ Wl.weight.detach().cpu().numpy().astype(np.float64)
     np.testing.assert_allclose(feats[0].grad.cpu().numpy(), dleft, rtol=1e-3, atol=1e-5)
     assert fuse.grad is None or float(fuse.grad.abs().max()) == 0.0
+
+
+# ---------------------------------------------------------------------------- AlignmentModule
+ALIGN_FIX = os.path.join(GOLD, "heads_align_B3_T12.npz")
+
+
+def _align_params(f):
+    return {k[6:]: f[k] for k in f if k.startswith("param.")}
+
+
+def test_oracle_alignment_matches_reference():
+    f = _load(ALIGN_FIX)
+    out, dx, grads = O.alignment_module(_align_params(f), f["x"], 2, True, G=f["G"])
+    np.testing.assert_allclose(out, f["out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(dx, f["dx"], rtol=1e-4, atol=1e-5)
+    for k, g in grads.items():
+        np.testing.assert_allclose(g, f["grad." + k], rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def _hip_alignment(params, x, G, hidden, cls):
+    from scattennet_amd.alignment import AlignmentModule
+    m = AlignmentModule(cls, x.shape[-1], hidden, num_layers=2, dropout=0.3, bidirectional=True).cuda().eval()
+    m.load_state_dict({k: torch.tensor(v) for k, v in params.items()})
+    xt = torch.tensor(x, device="cuda", requires_grad=True)
+    out = m(xt)
+    (out * torch.tensor(G, device="cuda")).sum().backward()
+    torch.cuda.synchronize()
+    return out.detach().cpu().numpy(), xt.grad.cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in
+                                                                m.named_parameters()}
+
+
+@pytest.mark.gpu
+def test_hip_alignment_matches_reference():
+    f = _load(ALIGN_FIX)
+    out, dx, grads = _hip_alignment(_align_params(f), f["x"], f["G"], 64, 20)
+    np.testing.assert_allclose(out, f["out"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(dx, f["dx"], rtol=1e-4, atol=2e-5)
+    for k, g in grads.items():
+        np.testing.assert_allclose(g, f["grad." + k], rtol=1e-4, atol=2e-5, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_hip_alignment_phoenix_size_matches_oracle():
+    """The yaml's head (input 1024, hidden 1024 = 2 x 512, 2 layers) at B = 4, T/4 = 64."""
+    torch.manual_seed(0)
+    from scattennet_amd.alignment import AlignmentModule
+    ref = AlignmentModule(300, 1024, 1024)
+    params = {k: v.numpy() for k, v in ref.state_dict().items()}
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((64, 4, 1024)).astype(np.float32)
+    G = rng.standard_normal((4, 64, 300)).astype(np.float32)
+    o_out, o_dx, o_grads = O.alignment_module(params, x, 2, True, G=G)
+    out, dx, grads = _hip_alignment(params, x, G, 1024, 300)
+    np.testing.assert_allclose(out, o_out, rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(dx, o_dx, rtol=1e-3, atol=1e-4)
+    for k, g in grads.items():
+        scale = float(np.abs(o_grads[k]).max())
+        np.testing.assert_allclose(g, o_grads[k], rtol=1e-3, atol=1e-4 * max(scale, 1.0), err_msg=k)
