@@ -24,6 +24,11 @@ from . import _lib as L
 from . import ops
 from .ops import _prob, _seg, gemm
 
+# split-K of the per-step recurrent GEMMs (M = B rows only): forward K = H, backward K = 4H
+# would otherwise run on N/64 workgroups per direction
+_SPLITK_FWD = int(__import__("os").environ.get("SCA_LSTM_SPLITK_FWD", "8"))
+_SPLITK_BWD = int(__import__("os").environ.get("SCA_LSTM_SPLITK_BWD", "16"))
+
 
 class LSTMLayer(Function):
     """One (bi)directional LSTM layer: x (B, T, In) -> y (B, T, D*H)."""
@@ -43,6 +48,7 @@ class LSTMLayer(Function):
         c = x.new_empty(B, T, D * H)
         y = x.new_empty(B, T, D * H)
         gt = x.new_empty(B, D * 4 * H)
+        ws = x.new_empty(_SPLITK_FWD * D * (B * 4 * H + B)) if _SPLITK_FWD > 1 else None
         lib, st = L.lib(), L.stream_handle()
         for step in range(T):
             probs = []
@@ -50,7 +56,7 @@ class LSTMLayer(Function):
                 t = step if d == 0 else T - 1 - step
                 probs.append(_prob([_seg(hp[:, t, d * H:], w_hh[d], T * D * H, H, H)], gt[:, d * 4 * H:], B, 4 * H,
                                    D * 4 * H, bias=b_hh[d], resid=G[:, t, d * 4 * H:], ldr=T * D * 4 * H))
-            gemm(L.GEMM_NT, probs)
+            gemm(L.GEMM_NT, probs, splitk=_SPLITK_FWD, ws=ws)
             L.check(lib.sca_lstm_cell_fwd(L.ptr(gt), L.ptr(G), L.ptr(c), L.ptr(y), L.ptr(hp), B, T, H, D, step, st),
                     "sca_lstm_cell_fwd")
         ctx.D = D
@@ -68,6 +74,7 @@ class LSTMLayer(Function):
         dG = x.new_empty(B, T, D * 4 * H)
         dh = x.new_empty(B, D * H)
         dc = x.new_empty(B, D * H)
+        ws = x.new_empty(_SPLITK_BWD * D * (B * H + B)) if _SPLITK_BWD > 1 else None
         lib, st = L.lib(), L.stream_handle()
         for step in range(T):
             if step > 0:
@@ -77,7 +84,7 @@ class LSTMLayer(Function):
                     tp = t + 1 if d == 0 else t - 1  # the frame the previous step processed
                     probs.append(_prob([_seg(dG[:, tp, d * 4 * H:], w_hh[d], T * D * 4 * H, H, 4 * H)],
                                        dh[:, d * H:], B, H, D * H, resid=dy[:, t, d * H:], ldr=T * D * H))
-                gemm(L.GEMM_NN, probs)
+                gemm(L.GEMM_NN, probs, splitk=_SPLITK_BWD, ws=ws)
             L.check(lib.sca_lstm_cell_bwd(L.ptr(dh) if step > 0 else None, L.ptr(dy), L.ptr(act), L.ptr(c),
                                           L.ptr(dc), L.ptr(dG), B, T, H, D, step, st), "sca_lstm_cell_bwd")
         dGf = dG.view(B * T, D * 4 * H)
