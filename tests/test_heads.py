@@ -237,3 +237,12 @@ def test_hip_alignment_phoenix_size_matches_oracle():
     for k, g in grads.items():
         scale = float(np.abs(o_grads[k]).max())
         np.testing.assert_allclose(g, o_grads[k], rtol=1e-3, atol=1e-4 * max(scale, 1.0), err_msg=k)
+
+
+def test_alignment_state_dict_keys_match_reference():
+    """Drop-in boundary: the reference's AlignmentModule parameter names (from its fixture) load strictly."""
+    from scattennet_amd.alignment import AlignmentModule
+    f = _load(ALIGN_FIX)
+    m = AlignmentModule(20, 64, 64, num_layers=2, dropout=0.3, bidirectional=True)
+    m.load_state_dict({k: torch.tensor(v) for k, v in _align_params(f).items()}, strict=True)
+    assert set(m.state_dict()) == set(_align_params(f))
