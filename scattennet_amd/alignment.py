@@ -30,6 +30,20 @@ _SPLITK_FWD = int(__import__("os").environ.get("SCA_LSTM_SPLITK_FWD", "8"))
 _SPLITK_BWD = int(__import__("os").environ.get("SCA_LSTM_SPLITK_BWD", "16"))
 
 
+def _stepper(template, a_step, r_step):
+    """Per-step problem builder: a copy of `template` (the step-0 problem) with the A operand
+    and residual pointers advanced by a_step / r_step bytes per step — the recurrent loop
+    then costs a struct copy per launch instead of tensor slicing + _prob (host-bound)."""
+    a0, r0 = template.seg[0].A, template.resid
+
+    def at(k):
+        p = L.GemmProblem.from_buffer_copy(template)
+        p.seg[0].A = a0 + k * a_step
+        p.resid = r0 + k * r_step
+        return p
+    return at
+
+
 class LSTMLayer(Function):
     """One (bi)directional LSTM layer: x (B, T, In) -> y (B, T, D*H)."""
 
@@ -50,13 +64,14 @@ class LSTMLayer(Function):
         gt = x.new_empty(B, D * 4 * H)
         ws = x.new_empty(_SPLITK_FWD * D * (B * 4 * H + B)) if _SPLITK_FWD > 1 else None
         lib, st = L.lib(), L.stream_handle()
+        steppers = []
+        for d in range(D):
+            t0, dt = (0, 1) if d == 0 else (T - 1, -1)
+            tpl = _prob([_seg(hp[:, t0, d * H:], w_hh[d], T * D * H, H, H)], gt[:, d * 4 * H:], B, 4 * H, D * 4 * H,
+                        bias=b_hh[d], resid=G[:, t0, d * 4 * H:], ldr=T * D * 4 * H)
+            steppers.append(_stepper(tpl, 4 * dt * D * H, 4 * dt * D * 4 * H))
         for step in range(T):
-            probs = []
-            for d in range(D):
-                t = step if d == 0 else T - 1 - step
-                probs.append(_prob([_seg(hp[:, t, d * H:], w_hh[d], T * D * H, H, H)], gt[:, d * 4 * H:], B, 4 * H,
-                                   D * 4 * H, bias=b_hh[d], resid=G[:, t, d * 4 * H:], ldr=T * D * 4 * H))
-            gemm(L.GEMM_NT, probs, splitk=_SPLITK_FWD, ws=ws)
+            gemm(L.GEMM_NT, [f(step) for f in steppers], splitk=_SPLITK_FWD, ws=ws)
             L.check(lib.sca_lstm_cell_fwd(L.ptr(gt), L.ptr(G), L.ptr(c), L.ptr(y), L.ptr(hp), B, T, H, D, step, st),
                     "sca_lstm_cell_fwd")
         ctx.D = D
@@ -76,15 +91,17 @@ class LSTMLayer(Function):
         dc = x.new_empty(B, D * H)
         ws = x.new_empty(_SPLITK_BWD * D * (B * H + B)) if _SPLITK_BWD > 1 else None
         lib, st = L.lib(), L.stream_handle()
+        steppers = []
+        for d in range(D):  # step 1: t = T-2 / 1, reading dG of the frame step 0 processed
+            t1, dt = (T - 2, -1) if d == 0 else (1, 1)
+            if T < 2:
+                break
+            tpl = _prob([_seg(dG[:, t1 - dt, d * 4 * H:], w_hh[d], T * D * 4 * H, H, 4 * H)], dh[:, d * H:], B, H,
+                        D * H, resid=dy[:, t1, d * H:], ldr=T * D * H)
+            steppers.append(_stepper(tpl, 4 * dt * D * 4 * H, 4 * dt * D * H))
         for step in range(T):
             if step > 0:
-                probs = []
-                for d in range(D):
-                    t = T - 1 - step if d == 0 else step
-                    tp = t + 1 if d == 0 else t - 1  # the frame the previous step processed
-                    probs.append(_prob([_seg(dG[:, tp, d * 4 * H:], w_hh[d], T * D * 4 * H, H, 4 * H)],
-                                       dh[:, d * H:], B, H, D * H, resid=dy[:, t, d * H:], ldr=T * D * H))
-                gemm(L.GEMM_NN, probs, splitk=_SPLITK_BWD, ws=ws)
+                gemm(L.GEMM_NN, [f(step - 1) for f in steppers], splitk=_SPLITK_BWD, ws=ws)
             L.check(lib.sca_lstm_cell_bwd(L.ptr(dh) if step > 0 else None, L.ptr(dy), L.ptr(act), L.ptr(c),
                                           L.ptr(dc), L.ptr(dG), B, T, H, D, step, st), "sca_lstm_cell_bwd")
         dGf = dG.view(B * T, D * 4 * H)
