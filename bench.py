@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from scattennet_amd import ops, workloads as W  # noqa: E402
-from scattennet_amd.dp import GradAllReduce  # noqa: E402
+from scattennet_amd.dp import GradBuckets  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA == fp32 vector peak
 HBM_PEAK_GBS = 8000.0
@@ -55,7 +55,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("SCA_DIST_BACKEND", "nccl") != "nccl":  # rehearsal: ranks may share a GPU
         local %= max(1, torch.cuda.device_count())
-    if world > 1:
+    # SCA_DP_FORCE=1 (under torch.distributed.run): the data-parallel path at world size 1 —
+    # rehearses the captured bucketed RCCL all-reduces on a one-GPU box
+    use_dp = world > 1 or ("MASTER_ADDR" in os.environ and os.environ.get("SCA_DP_FORCE", "0") != "0")
+    if use_dp:
         torch.cuda.set_device(local)
         backend = os.environ.get("SCA_DIST_BACKEND", "nccl")  # nccl == RCCL; gloo: rehearse N>1 on one GPU
         if backend == "nccl":
@@ -80,8 +83,11 @@ def main():
             dist.broadcast(p.data, 0)
     kp, mask, gout = W.synthetic_batch(w, dev, seed=1 + rank)
     grads_out = [gout[g].contiguous() for g in range(gout.shape[0])]
-    allreduce = GradAllReduce(model.parameters(), world)
     params = [p for p in model.parameters()]
+    # data parallel: gradients land in ~25 MB flat buckets whose RCCL all-reduces are issued
+    # from the backward as each bucket fills (captured into the step's hipGraph); gloo
+    # rehearsals all-reduce the buckets after the step instead (reducer.sync)
+    reducer = GradBuckets(params, world) if use_dp else None
 
     def fwd_bwd():
         if args.dropout > 0:
@@ -90,9 +96,13 @@ def main():
         outs = outs[:1] if fusion else outs  # config 3: the loss seed sits on the fusion output
         torch.autograd.backward(outs, grads_out)
 
+    def sync():
+        if reducer is not None:
+            reducer.sync()
+
     def step():
         fwd_bwd()
-        allreduce()
+        sync()
 
     # warm-up (also builds the library's lazy state) on a side stream, as graph capture requires
     s = torch.cuda.Stream(device=dev)
@@ -105,44 +115,55 @@ def main():
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
 
-    # the captured graph holds forward + backward (~200 HIP launches); the RCCL gradient
-    # all-reduce (N > 1) runs eagerly right after each replay on the same stream
+    # the captured graph holds forward + backward (~200 HIP launches) and, with RCCL, the
+    # bucketed gradient all-reduces overlapped with the backward
     graph = None
     if not args.no_graph:
         for p in params:
             p.grad = None
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture mode with RCCL: ProcessGroupNCCL's watchdog thread queries the
+        # warm-up steps' events while the step is captured (tools/dp_capture_diag.py)
+        with torch.cuda.graph(graph, capture_error_mode="thread_local" if reducer is not None else "global"):
             fwd_bwd()
         for _ in range(2):
             graph.replay()
-            allreduce()
+            sync()
         torch.cuda.synchronize()
+
+    marks = []
 
     def run(k):
         for _ in range(k):
             if graph is not None:
                 graph.replay()
-                allreduce()
+                sync()
             else:
                 for p in params:
                     p.grad = None
                 step()
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            marks.append(ev)
 
-    if world > 1:
+    if use_dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    start = torch.cuda.Event(enable_timing=True)
+    start.record()
     run(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dp:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_dp:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = 1000.0 * elapsed / args.steps
+    per_step = sorted(a.elapsed_time(b) for a, b in zip([start] + marks[:-1], marks))
+    ms_median = per_step[len(per_step) // 2]
     clips = w["B"] * world * args.steps / elapsed
     step_flops = W.flops_per_step(w)
 
@@ -185,11 +206,18 @@ def main():
                        "joints": w["K_all"], "streams": w["groups"], "d_model": w["d"], "heads": w["H"],
                        "layers": w["L"], "dropout": args.dropout, "hipgraph": graph is not None,
                        "parallelism": f"dp{world}"},
+            "ms_per_step_median": round(ms_median, 4),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if reducer is not None:
+            line["config"]["grad_allreduce"] = {
+                "backend": dist.get_backend(), "buckets_mb": [round(b / 2 ** 20, 2) for b in reducer.bucket_sizes()],
+                "overlapped": reducer.overlap, "in_graph": reducer.overlap and graph is not None,
+                "fallback_params": len(reducer.last_fallback)}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dp:
+        reducer.close()
         dist.destroy_process_group()
 
 

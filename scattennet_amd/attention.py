@@ -50,19 +50,42 @@ class BaseAttention(nn.Module):
                 self.v_proj.weight, self.v_proj.bias]
 
 
-def _resolve_mask(mask, causal):
-    """-> (key_valid, add_mask, plus_one)."""
+def _resolve_mask(mask, causal, B, Tq, Tk, device):
+    """-> (key_valid, add_mask, plus_one).
+
+    The kernels read `add_mask` as a dense contiguous (B, Tq, Tk) fp32 buffer and
+    `key_valid` as (B, Tk).  The reference adds the mask with `attn_weights += attention_mask`
+    (attention.py:65/117/171), so every mask broadcastable to (B, 1, Tq, Tk) is legal there:
+    (B,1,Tq,Tk), (1,1,Tq,Tk), (B,1,1,Tk), (Tq,Tk), (Tk,), a scalar ...  Such masks are
+    expanded to (B, Tq, Tk) here; per-head masks (dim 1 = H > 1) are not supported
+    (ValueError).  `None` raises TypeError as `attn_weights += None` does."""
     if mask is None:
-        return None, None, False
+        raise TypeError("unsupported operand type(s) for +=: 'Tensor' and 'NoneType'")
     if isinstance(mask, ops.KeyPaddingMask):
-        return mask.key_valid, None, bool(causal and mask.causal_plus_one)
+        kv = mask.key_valid
+        if tuple(kv.shape) != (B, Tk):
+            raise ValueError(f"key padding mask is {tuple(kv.shape)}, expected (B, Tk) = {(B, Tk)}")
+        if kv.device != device:
+            raise RuntimeError(f"key padding mask on {kv.device}, queries on {device}")
+        return kv, None, bool(causal and mask.causal_plus_one)
     if torch.is_tensor(mask):
         m = mask
-        if m.dim() == 4:
-            if m.shape[1] != 1:
-                raise ValueError("attention_mask must be (B, 1, Tq, Tk)")
-            m = m[:, 0]
-        return None, m.to(torch.float32).contiguous(), False
+        if m.dim() > 4:
+            raise ValueError(f"attention_mask of shape {tuple(m.shape)} does not broadcast to (B, H, Tq, Tk)")
+        if m.device != device:
+            if m.dim() != 0:  # as in the reference, only a 0-dim CPU tensor may meet a device tensor
+                raise RuntimeError(f"attention_mask on {m.device}, queries on {device}")
+            m = m.to(device)
+        m = m.reshape((1,) * (4 - m.dim()) + tuple(m.shape))
+        if m.shape[1] != 1:
+            raise ValueError(f"attention_mask of shape {tuple(mask.shape)}: per-head masks are not supported "
+                             "(dim 1 must be 1)")
+        for have, want, name in ((m.shape[0], B, "B"), (m.shape[2], Tq, "Tq"), (m.shape[3], Tk, "Tk")):
+            if have not in (1, want):
+                raise ValueError(f"attention_mask of shape {tuple(mask.shape)} does not broadcast to "
+                                 f"(B, 1, Tq, Tk) = {(B, 1, Tq, Tk)} ({name})")
+        m = m.to(torch.float32).expand(B, 1, Tq, Tk)[:, 0]
+        return None, m.contiguous(), False
     raise TypeError(f"unsupported attention_mask type {type(mask)}")
 
 
@@ -80,7 +103,11 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
         if a.training and a.dropout > 0:
             raise NotImplementedError("attention dropout > 0 in training mode is not implemented")
     causal = kind == "causal"
-    key_valid, add_mask, plus_one = _resolve_mask(mask, causal)
+    hq = hidden[0]
+    if hq.dim() != 3:
+        raise ValueError(f"hidden_states must be (B, T, d_model), got {tuple(hq.shape)}")
+    Tk = kv[0].shape[1] if kind == "cross" else hq.shape[1]
+    key_valid, add_mask, plus_one = _resolve_mask(mask, causal, hq.shape[0], hq.shape[1], Tk, hq.device)
     params = []
     for a in attns:
         params += a.qkv_params()

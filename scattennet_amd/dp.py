@@ -3,46 +3,252 @@
 The reference initialises an NCCL process group but never wraps the model in DDP nor
 all-reduces a gradient (utils.py:237-265, main.py:132-133), so this is the
 north-star's new functionality: one process per GPU, each running its own clips through the
-HIP path, and ONE coalesced fp32 all-reduce of all gradients per step over RCCL/xGMI
-(torch.distributed backend "nccl" is RCCL on ROCm).  The 4-stream SCA has 25.8 M
-parameters: one 103 MB bucket, which RCCL splits over its channels / all 7 xGMI links.
+HIP path, the fp32 gradients averaged over all ranks every step (torch.distributed backend
+"nccl" is RCCL on ROCm).
+
+`GradBuckets` is the reducer.  It installs itself as the parameter-gradient sink of
+`ops` (ops.param_grad_empty / ops.params_produced):
+
+* Plan.  The first backward runs unbucketed and records the order in which the backward
+  produces parameter gradients.  The gradients are then laid out in that order in ONE flat
+  fp32 buffer, cut into buckets of about `bucket_mb` MB (default 25: four buckets for the
+  103 MB of the 4-stream SCA) — the bucket holding the top layers' gradients fills first.
+  Parameters that never receive a gradient (the ResidualNetwork long shortcuts, SURVEY.md
+  §7) get no slot and keep `.grad = None`, as in the reference; so do parameters whose
+  gradient arrives in more than one piece (autograd would add the pieces outside our
+  streams) and parameters produced outside the `ops` sites — those are reduced by a
+  fallback all-reduce after the backward.
+* Steps.  Every kernel writing a planned gradient writes straight into that parameter's
+  slot (no flatten / copy-back), and `.grad` is left as a view of the slot.  With the
+  overlapped mode (RCCL), the moment a bucket's last gradient has been enqueued, the
+  bucket's all-reduce is issued on a communication stream that waits on exactly the
+  streams that produced its gradients (the weight-gradient side streams), so it runs under
+  the backward of the layers below; the caller's stream joins the communication stream when
+  the backward completes (an autograd final callback).  All of this is capture-safe: the
+  bench captures forward + backward + the bucketed all-reduces in one hipGraph.
+  Without overlap (the `gloo` rehearsal backend, or SCA_DP_OVERLAP=0), `sync()` after the
+  backward (or graph replay) all-reduces the flat buffer in place.
+* Averaging: each bucket is pre-scaled by 1/world on the communication stream, then SUM
+  all-reduced (exact for power-of-two world sizes).
 
 Oracle: the averaged all-reduced gradient times the world size equals the single-process
-gradient of the whole global batch (sum loss) — tests/test_dp.py checks it with `gloo`.
-Parameters that never receive a gradient (the ResidualNetwork long shortcuts) are reduced
-as zeros and left without a .grad, as in the reference.
+gradient of the whole global batch (sum loss) — tests/test_dp.py checks the reducer with
+`gloo`; tests/test_gpu_dp.py checks batch additivity of the HIP gradients and the captured
+bucketed path at world size 1 on RCCL.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
+from . import ops
 
-class GradAllReduce:
-    """Average the gradients of `params` over all ranks with one coalesced all-reduce.
+_ALIGN = 64  # floats: every slot starts on a 256-byte boundary
 
-    Flatten (one cat launch), all-reduce, scatter back (one multi-tensor copy launch); the
-    set of parameters holding a gradient is structural (identical on every rank)."""
 
-    def __init__(self, params, world=None, average=True):
+class GradBuckets:
+    def __init__(self, params, world=None, bucket_mb=None, overlap=None, average=True):
         self.params = [p for p in params if p.requires_grad]
         self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
         self.average = average
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.empty(n, device=self.params[0].device, dtype=torch.float32)
+        self.bucket_bytes = int(float(bucket_mb if bucket_mb is not None else
+                                      os.environ.get("SCA_DP_BUCKET_MB", "25")) * 2 ** 20)
+        backend = dist.get_backend() if dist.is_initialized() else None
+        if overlap is None:
+            overlap = backend == "nccl" and os.environ.get("SCA_DP_OVERLAP", "1") != "0"
+        self.overlap = bool(overlap)
+        # issue the collectives even at world size 1 (SCA_DP_FORCE=1: rehearse the captured
+        # RCCL path on a one-GPU box; the all-reduce is then an identity)
+        self.collective = self.world > 1 or (dist.is_initialized() and os.environ.get("SCA_DP_FORCE", "0") != "0")
+        self._key = {self._k(p): i for i, p in enumerate(self.params)}
+        self.plan = None          # list of buckets: (offset, numel, [param indices])
+        self.flat = None
+        self.slot = {}            # param index -> (offset, numel)
+        self.bucket_of = {}       # param index -> bucket index
+        self._order, self._count = [], {}
+        self._comm = None
+        self._step = None
+        self.last_fallback = []   # parameter indices reduced by the fallback in the last step
+        ops.set_grad_sink(self)
 
-    def __call__(self):
-        if self.world == 1:
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _k(p):
+        return (p.data_ptr(), p.numel())
+
+    def _index(self, p):
+        return self._key.get(self._k(p))
+
+    def close(self):
+        if ops._GRAD_SINK is self:
+            ops.set_grad_sink(None)
+
+    def _stream(self):
+        return torch.cuda.current_stream() if self.params[0].is_cuda else None
+
+    def _begin(self):
+        """First sink call of a backward: choose this step's mode and queue its finish."""
+        fast = self.plan is not None and all(self.params[i].grad is None for i in self.slot)
+        self._step = {"fast": fast, "pending": [len(b[2]) for b in self.plan] if fast else None,
+                      "streams": [dict() for _ in self.plan] if fast else None, "works": [],
+                      "seen": set(), "producers": {}}
+        torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+
+    # ------------------------------------------------------------------ sink protocol (ops)
+    def grad_buffer(self, p):
+        if self._step is None:
+            self._begin()
+        if not self._step["fast"]:
+            return None
+        i = self._index(p)
+        if i is None or i not in self.slot or p.grad is not None:
+            return None
+        o, n = self.slot[i]
+        return self.flat[o:o + n].view(p.shape)
+
+    def produced(self, params):
+        if self._step is None:
+            self._begin()
+        st = self._step
+        stream = self._stream()
+        if stream is not None:
+            st["producers"][stream.cuda_stream] = stream
+        for p in params:
+            i = self._index(p)
+            if i is None:
+                continue
+            if self.plan is None:  # discovery step: record the production order
+                if i not in self._count:
+                    self._order.append(i)
+                self._count[i] = self._count.get(i, 0) + 1
+                continue
+            if not st["fast"] or i not in self.slot or i in st["seen"]:
+                continue
+            st["seen"].add(i)
+            b = self.bucket_of[i]
+            if stream is not None:
+                st["streams"][b][stream.cuda_stream] = stream
+            st["pending"][b] -= 1
+            if st["pending"][b] == 0 and self.overlap and self.collective:
+                self._launch(b)
+
+    # ------------------------------------------------------------------ collectives
+    def _bucket(self, b):
+        o, n, _ = self.plan[b]
+        return self.flat[o:o + n]
+
+    def _comm_stream(self):
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=self.params[0].device)
+        return self._comm
+
+    def _launch(self, b):
+        """Average = pre-scale by 1/world (exact for power-of-two worlds) + SUM all-reduce.
+        The collective is issued from the communication stream (forked from the producers)
+        and waited on by the CALLER's stream at the end of the backward: under hipGraph
+        capture, RCCL's stream may fork from a side stream but must join the capture's
+        origin stream — a wait on it from a forked stream crashes graph instantiation on
+        this ROCm (tools/dp_capture_diag.py: variants "kernel" vs "mainwait")."""
+        if not self.params[0].is_cuda:  # CPU tensors (gloo tests)
+            if self.average:
+                self._bucket(b).mul_(1.0 / self.world)
+            self._step["works"].append(dist.all_reduce(self._bucket(b), async_op=True))
             return
-        grads = [p.grad for p in self.params if p.grad is not None]
-        if not grads:
+        comm = self._comm_stream()
+        for s in self._step["streams"][b].values():
+            comm.wait_stream(s)  # the bucket's gradients are enqueued on these streams
+        with torch.cuda.stream(comm):
+            if self.average:
+                self._bucket(b).mul_(1.0 / self.world)
+            self._step["works"].append(dist.all_reduce(self._bucket(b), async_op=True))
+
+    def _finish(self):
+        st, self._step = self._step, None
+        if st is None:
             return
-        n = sum(g.numel() for g in grads)
-        flat = self.flat[:n]
-        torch.cat([g.reshape(-1) for g in grads], out=flat)
+        # this callback may run before the weight-gradient side streams' own join callbacks:
+        # order the caller's stream after every stream that produced a gradient
+        cur = self._stream()
+        if cur is not None:
+            for s in st["producers"].values():
+                if s.cuda_stream != cur.cuda_stream:
+                    cur.wait_stream(s)
+        if self.plan is None:
+            self._build_plan()
+            self._fallback(list(range(len(self.params))))
+            return
+        if not st["fast"]:  # .grad already held gradients (accumulation): reduce them as they are
+            self._fallback(list(range(len(self.params))))
+            return
+        missing = [b for b, n in enumerate(st["pending"]) if n != 0]
+        if missing:
+            raise RuntimeError(f"GradBuckets: buckets {missing} did not receive all their gradients this step "
+                               "(the parameter set producing gradients changed after the first step)")
+        for i, (o, n) in self.slot.items():  # .grad is the slot (whether or not autograd stole the view)
+            p = self.params[i]
+            if p.grad is None or p.grad.data_ptr() != self.flat[o:].data_ptr():
+                p.grad = self.flat[o:o + n].view(p.shape)
+        for work in st["works"]:
+            work.wait()  # GPU: the caller's stream waits for RCCL's stream; CPU: completes it
+        self._fallback([i for i, p in enumerate(self.params) if i not in self.slot and p.grad is not None])
+
+    def _build_plan(self):
+        planned = [i for i in self._order if self._count[i] == 1]
+        off, cur, buckets = 0, [], []
+        start = 0
+        for i in planned:
+            n = self.params[i].numel()
+            if cur and (off + n - start) * 4 > self.bucket_bytes:
+                buckets.append((start, off - start, cur))
+                start, cur = off, []
+            self.slot[i] = (off, n)
+            cur.append(i)
+            off += -(-n // _ALIGN) * _ALIGN
+        if cur:
+            buckets.append((start, off - start, cur))
+        self.plan = buckets
+        for b, (_, _, idx) in enumerate(buckets):
+            for i in idx:
+                self.bucket_of[i] = b
+        self.flat = torch.zeros(max(off, 1), device=self.params[0].device, dtype=torch.float32)
+
+    def _fallback(self, idx):
+        """All-reduce (and average) the gradients of parameters `idx` that hold one, in one
+        flattened collective, on the current stream."""
+        self.last_fallback = [i for i in idx if self.params[i].grad is not None]
+        if not self.collective or not self.last_fallback:
+            return
+        grads = [self.params[i].grad for i in self.last_fallback]
+        flat = torch.cat([g.reshape(-1) for g in grads])
         dist.all_reduce(flat)
         if self.average:
             flat.mul_(1.0 / self.world)
-        views, o = [], 0
+        o = 0
         for g in grads:
-            views.append(flat[o:o + g.numel()].view_as(g))
+            g.copy_(flat[o:o + g.numel()].view_as(g))
             o += g.numel()
-        torch._foreach_copy_(grads, views)
+
+    # ------------------------------------------------------------------ non-overlapped mode
+    def sync(self):
+        """Without overlap: all-reduce the planned gradients (the flat buffer, in place) after
+        the backward / graph replay.  A no-op in the overlapped mode or at world size 1."""
+        if not self.collective:
+            return
+        if self.plan is None:  # no backward went through the ops sites: reduce .grad as it is
+            self._fallback(list(range(len(self.params))))
+            return
+        if self.overlap:
+            return
+        dist.all_reduce(self.flat)
+        if self.average:
+            self.flat.mul_(1.0 / self.world)
+
+    def bucket_sizes(self):
+        return [n * 4 for _, n, _ in (self.plan or [])]
+
+
+class GradAllReduce(GradBuckets):
+    """Back-compatible name: the bucketed reducer, called after each step (`reducer()`)."""
+
+    def __call__(self):
+        self.sync()

@@ -85,18 +85,35 @@ class CTCLossOp(Function):
         return dx, None, None, None
 
 
-def _validate_ctc(labels, tgt_lengths, input_lengths, T, C):
-    """torch.nn.CTCLoss's argument checks (as the reference's CPU call raises them), done on
-    the host only for CPU tensors — never a device sync."""
-    if labels.dim() != 2:
-        raise RuntimeError("scattennet_amd compute_loss: labels must be (B, S) padded")
-    if isinstance(tgt_lengths, torch.Tensor) and tgt_lengths.device.type == "cpu":
-        S_eff = tgt_lengths.clamp(min=1)
+def _host_lengths(t):
+    """Lengths as a host tensor for validation, or None when that would need a device sync
+    under hipGraph capture (the kernels' clamps then keep a bad call in bounds)."""
+    t = torch.as_tensor(t)
+    if t.device.type == "cpu":
+        return t
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    return t.cpu()  # one sync, as the reference's own .cpu() of the lengths (model/__init__.py:265-269)
+
+
+def _validate_ctc(labels, tgt_lengths, input_lengths, B, T, C):
+    """torch.nn.CTCLoss's argument checks (as the reference's call raises them): labels (B, S)
+    padded, one input / target length per clip, target lengths <= S, input lengths <= T,
+    labels in [0, C)."""
+    if labels.dim() != 2 or labels.shape[0] != B:
+        raise RuntimeError(f"scattennet_amd compute_loss: labels must be (B, S) padded with B = {B}, "
+                           f"got {tuple(labels.shape)}")
+    for name, t in (("target_lengths", tgt_lengths), ("input_lengths", input_lengths)):
+        if torch.as_tensor(t).numel() != B:
+            raise RuntimeError(f"Expected {name} to have {B} entries (one per clip), got {torch.as_tensor(t).numel()}")
+    tl, il = _host_lengths(tgt_lengths), _host_lengths(input_lengths)
+    if tl is not None:
+        S_eff = tl.clamp(min=1)
         if int(S_eff.max()) > labels.shape[1]:
             raise RuntimeError(f"Expected tensor to have size at least {int(S_eff.max())} at dimension 1, "
                                f"but got size {labels.shape[1]} for argument #2 'targets'")
-        if isinstance(input_lengths, torch.Tensor) and input_lengths.device.type == "cpu":
-            T_eff = torch.maximum(input_lengths.clamp(min=1), S_eff)
+        if il is not None:
+            T_eff = torch.maximum(il.clamp(min=1), S_eff)
             if int(T_eff.max()) > T:
                 raise RuntimeError(f"Expected input_lengths to have value at most {T}, but got value "
                                    f"{int(T_eff.max())}")
@@ -106,14 +123,38 @@ def _validate_ctc(labels, tgt_lengths, input_lengths, T, C):
             raise RuntimeError(f"target values must lie in [0, {C}); got [{lo}, {hi}]")
 
 
+def _pad_concatenated(labels, tgt_lengths, B):
+    """nn.CTCLoss's 1-D form: the targets of all clips concatenated, split by the target
+    lengths as the reference passes them (clamped to >= 1, model/__init__.py:263) ->
+    (B, max S) padded."""
+    tl = _host_lengths(tgt_lengths)
+    if tl is None:
+        raise RuntimeError("compute_loss: 1-D (concatenated) labels need host-visible target lengths under "
+                           "graph capture; pass (B, S) padded labels")
+    tl = tl.reshape(-1).clamp(min=1).to(torch.int64)
+    if tl.numel() != B:
+        raise RuntimeError(f"Expected target_lengths to have {B} entries (one per clip), got {tl.numel()}")
+    total = int(tl.sum())
+    if labels.numel() < total:
+        raise RuntimeError(f"concatenated targets hold {labels.numel()} labels, target_lengths sum to {total}")
+    out = labels.new_zeros(B, int(tl.max()))
+    o = 0
+    for b in range(B):
+        n = int(tl[b])
+        out[b, :n] = labels[o:o + n]
+        o += n
+    return out
+
+
 def compute_loss(labels, tgt_lengths, logits, input_lengths, return_per_sample=False):
     """MSCA_Net.compute_loss (model/__init__.py:241-290): logits (B, T, C) batch-major (the
-    reference permutes to (T, B, C) itself).  Returns the clamped mean CTC loss (0-dim)."""
+    reference permutes to (T, B, C) itself).  labels: (B, S) padded, or 1-D concatenated as
+    nn.CTCLoss also accepts.  Returns the clamped mean CTC loss (0-dim)."""
     B, T, C = logits.shape
     labels = torch.as_tensor(labels)
     if labels.dim() == 1:
-        labels = labels[None]
-    _validate_ctc(labels, torch.as_tensor(tgt_lengths), torch.as_tensor(input_lengths), T, C)
+        labels = _pad_concatenated(labels, tgt_lengths, B)
+    _validate_ctc(labels, tgt_lengths, input_lengths, B, T, C)
     dev = logits.device
     loss, nll = CTCLossOp.apply(logits, _dev_i32(labels, dev), _dev_i32(input_lengths, dev),
                                 _dev_i32(tgt_lengths, dev))

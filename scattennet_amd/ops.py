@@ -232,9 +232,10 @@ def _ln_bwd(dys, x, gam, means, rstds, defer_affine=False, params=None):
     N = x[0].shape[-1]
     rows = x[0].numel() // N
     nblk = L.lib().sca_layernorm_bwd_blocks(rows)
+    bet = params[G:] if params is not None and len(params) == 2 * G else [None] * G
     dx = [torch.empty_like(t) for t in x]
-    dg = [torch.empty_like(t) for t in gam]
-    db = [torch.empty_like(t) for t in gam]
+    dg = [param_grad_empty(t) for t in gam]
+    db = [param_grad_empty(bet[g]) if bet[g] is not None else torch.empty_like(gam[g]) for g in range(G)]
     part = [x[0].new_empty(2 * nblk * N) for _ in range(G)]
     for c in range(0, G, L.LN_MAX_PROBLEMS):
         gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
@@ -251,6 +252,8 @@ def _ln_bwd(dys, x, gam, means, rstds, defer_affine=False, params=None):
         finish = (lambda: reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
                                       [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0),
                   part, params or ())
+    else:
+        params_produced(params or ())
     return dx, dg, db, finish
 
 
@@ -294,6 +297,43 @@ _SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
 _WGRAD_MIX = __import__("os").environ.get("SCA_WGRAD_MIX", "0") != "0"
 _SPLITK_ROUNDS = __import__("os").environ.get("SCA_SPLITK_ROUNDS", "1") != "0"
 _SPLITK_SLOTS = int(__import__("os").environ.get("SCA_SPLITK_SLOTS", "768"))  # workgroup slots per round
+
+
+# ---- parameter-gradient sink -------------------------------------------------------------
+# Every backward below allocates a parameter's gradient through `param_grad_empty` and, once
+# the launches writing it are enqueued, reports it through `params_produced` (on the stream
+# that wrote it).  With no sink installed that is torch.empty_like and a no-op.  The data-
+# parallel reducer (dp.GradBuckets) installs itself as the sink: gradients are then written
+# straight into slots of its flat all-reduce buckets, and a bucket's RCCL all-reduce is
+# issued as soon as its last gradient has been enqueued — overlapped with the rest of the
+# backward.
+_GRAD_SINK = None
+
+
+def set_grad_sink(sink):
+    global _GRAD_SINK
+    _GRAD_SINK = sink
+
+
+def param_grad_empty(p):
+    if _GRAD_SINK is not None:
+        t = _GRAD_SINK.grad_buffer(p)
+        if t is not None:
+            return t
+    return torch.empty_like(p)
+
+
+def param_grad_zeros(p):
+    if _GRAD_SINK is not None:
+        t = _GRAD_SINK.grad_buffer(p)
+        if t is not None:
+            return t.zero_()
+    return torch.zeros_like(p)
+
+
+def params_produced(ps):
+    if _GRAD_SINK is not None:
+        _GRAD_SINK.produced([p for p in ps if p is not None and not isinstance(p, bool)])
 
 
 # ---- weight-gradient side stream -------------------------------------------------------
@@ -354,13 +394,16 @@ def weight_grads(items, M=None, extra=None):
     """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
     the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
 
-    items: list of (dY[M,out], X[M,in], alpha, W_like, has_bias[, bias_scale]) -> [(dW, db)].
-    bias_scale defaults to alpha; it differs when alpha scales the INPUT X (v from kv/2:
-    dWv = dV^T (kv/2) but dbv = colsum(dV))."""
+    items: list of (dY[M,out], X[M,in], alpha, W, bias[, bias_scale]) -> [(dW, db)]; W and
+    bias are the parameters (bias None / False: no bias gradient; True: a bias gradient
+    without its parameter at hand).  bias_scale defaults to alpha; it differs when alpha
+    scales the INPUT X (v from kv/2: dWv = dV^T (kv/2) but dbv = colsum(dV))."""
     def run():
         out = _weight_grads(items)
+        params_produced([p for it in items for p in (it[3], it[4])])
         if extra is not None:
             extra[0]()
+            params_produced(extra[2])
         return out
 
     # a parameter that already holds a .grad gets the new gradient added by autograd as soon
@@ -399,10 +442,13 @@ def _weight_grads(items):
     out = []
     by_shape = {}  # problems of one launch (SCA_WGRAD_MIX=1: any shapes, one launch)
     items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
-    for idx, (dY, X, alpha, W, has_bias, _) in enumerate(items):
+    for idx, (dY, X, alpha, W, bias, _) in enumerate(items):
         n_out, n_in = W.shape
-        dW = torch.empty_like(W)
-        db = torch.empty(n_out, device=W.device, dtype=W.dtype) if has_bias else None
+        dW = param_grad_empty(W)
+        if torch.is_tensor(bias):
+            db = param_grad_empty(bias)
+        else:
+            db = torch.empty(n_out, device=W.device, dtype=W.dtype) if bias else None
         out.append((dW, db))
         key = (n_out, n_in, dY.shape[0]) if not _WGRAD_MIX else dY.shape[0]
         by_shape.setdefault(key, []).append(idx)
@@ -559,6 +605,7 @@ class AttentionBlock(Function):
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
+        ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
         ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
                               *sm, *sl, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
@@ -589,7 +636,7 @@ class AttentionBlock(Function):
             i += 6 * G
             vs, gam, means, rstds = (sv[i + j * G:i + (j + 1) * G] for j in range(4))
             dys, dgam, dbet, ln_finish = _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE,
-                                                 params=gam)
+                                                 params=tuple(gam) + ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
         dyo = dys  # gradient of the out-projection output: the dropout mask applied to dY
         if ctx.drop_p > 0:
@@ -624,9 +671,9 @@ class AttentionBlock(Function):
         for g in range(G):
             Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
             xf, kf = _flat(xq[g]), _flat(xkv[g])
-            items += [(_flat(dq[g]), xf, 1.0, Wq, bq is not None), (_flat(dk[g]), kf, 1.0, Wk, bk is not None),
-                      (_flat(dv[g]), kf, 1.0, Wv, bv is not None, 1.0 / av),
-                      (_flat(dyo[g]), _flat(o[g]), 1.0, Wo[g], bo[g] is not None)]
+            items += [(_flat(dq[g]), xf, 1.0, Wq, bq), (_flat(dk[g]), kf, 1.0, Wk, bk),
+                      (_flat(dv[g]), kf, 1.0, Wv, bv, 1.0 / av),
+                      (_flat(dyo[g]), _flat(o[g]), 1.0, Wo[g], bo[g])]
         wg = weight_grads(items, extra=ln_finish)
         dW, dWo, dbo = [], [], []
         for g in range(G):
@@ -659,7 +706,7 @@ class LinearResidual(Function):
                                resid=r[g], ldr=n_out))
             ys.append(y)
         gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.has_r, ctx.has_b = G, has_r, [bb is not None for bb in b]
+        ctx.G, ctx.has_r, ctx.b = G, has_r, tuple(b)  # biases: parameters (leaves) or None
         ctx.save_for_backward(*x, *W)
         return tuple(ys)
 
@@ -677,7 +724,7 @@ class LinearResidual(Function):
             probs.append(_prob([_seg(_flat(dys[g]), W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
             dxs.append(dx)
         gemm(L.GEMM_NN, probs)
-        wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.has_b[g]) for g in range(G)])
+        wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
         return (None, None) + tuple(dxs) + tuple(w for w, _ in wg) + tuple(bb for _, bb in wg) + \
             (tuple(dys) if ctx.has_r else ())
 
@@ -720,6 +767,7 @@ class FeedForwardResidual(Function):
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
+        ctx.b1, ctx.b2, ctx.bet = tuple(b1), tuple(b2), (tuple(bet) if ln else ())  # parameters (leaves)
         ctx.save_for_backward(*x, *W1, *W2, *zs, *acts, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
 
@@ -734,7 +782,7 @@ class FeedForwardResidual(Function):
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             vs, gam, means, rstds = (sv[(5 + i) * G:(6 + i) * G] for i in range(4))
             dys, dgam, dbet, ln_finish = _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE,
-                                                 params=gam)
+                                                 params=tuple(gam) + ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
         B, T, d = x[0].shape
         M = B * T
@@ -752,8 +800,9 @@ class FeedForwardResidual(Function):
         dx = [torch.empty_like(x[g]) for g in range(G)]
         gemm(L.GEMM_NN, [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
                                resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)])
-        items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], True) for g in range(G)] + \
-                [(dz[g], _flat(x[g]), 1.0, W1[g], True) for g in range(G)]
+        items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], ctx.b2[g] if ctx.b2[g] is not None else True)
+                 for g in range(G)] + \
+                [(dz[g], _flat(x[g]), 1.0, W1[g], ctx.b1[g] if ctx.b1[g] is not None else True) for g in range(G)]
         wg = weight_grads(items, extra=ln_finish)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
@@ -804,6 +853,7 @@ class LayerNormAdd(Function):
                     "sca_layernorm_fwd")
         ctx.G, ctx.pos, ctx.has_post, ctx.act, ctx.r_mod, ctx.r_off = G, pos_table, has_post, act, r_mod, r_off
         ctx.drop_p, ctx.seeds = drop_p, seeds
+        ctx.bet = tuple(bet)  # parameters (leaves): identify their gradients' slots
         ctx.save_for_backward(*x, *(tab if pos_table else []), *gam, *means, *rstds, *(ys if act else []))
         return tuple(ys)
 
@@ -827,8 +877,8 @@ class LayerNormAdd(Function):
         nblk = L.lib().sca_layernorm_bwd_blocks(rows)
         dx = [torch.empty_like(t) for t in x]
         dpost = [torch.empty_like(t) for t in x] if ctx.has_post else [None] * G
-        dg = [torch.empty_like(t) for t in gam]
-        db = [torch.empty_like(t) for t in gam]
+        dg = [param_grad_empty(t) for t in gam]
+        db = [param_grad_empty(t) for t in ctx.bet]
         part = [x[0].new_empty(2 * nblk * N) for _ in range(G)]
         for c in range(0, G, L.LN_MAX_PROBLEMS):
             gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
@@ -839,12 +889,17 @@ class LayerNormAdd(Function):
                                                                 db[g].data_ptr(), part[g].data_ptr()) for g in gs])
             L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, ctx.r_mod, ctx.r_off, 0, L.stream_handle()),
                     "sca_layernorm_bwd")
+        params_produced(list(gam) + list(ctx.bet))
         dtab = []
         if pos:
             B, T = x[0].shape[0], x[0].shape[1]
-            dtab = list(torch.zeros((G,) + tuple(tab[0].shape), device=tab[0].device).unbind(0))  # one fill
+            if _GRAD_SINK is None:
+                dtab = list(torch.zeros((G,) + tuple(tab[0].shape), device=tab[0].device).unbind(0))  # one fill
+            else:
+                dtab = [param_grad_zeros(t) for t in tab]
             # d table[t + 2] = sum_b dv[b, t]
             reduce_rows([(dx[g], dtab[g][2:], 1.0) for g in range(G)], B, T, N, T * N, N)
+            params_produced(tab)
         return (None,) * 6 + tuple(dx) + tuple(dtab) + (tuple(dpost) if ctx.has_post else ()) + \
             tuple(dg) + tuple(db)
 
@@ -906,7 +961,7 @@ class CoordinateMappingOp(Function):
             L.check(L.lib().sca_coord_map_fwd(len(gs), arr, rows, K_all, N, L.stream_handle()), "sca_coord_map_fwd")
         ctx.G = G
         ctx.kp_grad = kp.requires_grad
-        ctx.has_b = [b is not None for b in bx]
+        ctx.bx, ctx.by = tuple(bx), tuple(by)  # parameters (leaves) or None
         ctx.save_for_backward(kpc, *idx, *Wx, *Wy)
         return tuple(xe) + tuple(ye)
 
@@ -922,8 +977,8 @@ class CoordinateMappingOp(Function):
         refs = [kp.new_empty(B, T, N)] * (2 * G)
         grads = _contig(_zeros_for_none(grads, refs))
         dxe, dye = grads[:G], grads[G:]
-        dwx = [torch.empty_like(w) for w in Wx]
-        dwy = [torch.empty_like(w) for w in Wy]
+        dwx = [param_grad_empty(w) for w in Wx]
+        dwy = [param_grad_empty(w) for w in Wy]
         dkp = torch.zeros_like(kp) if ctx.kp_grad else None
         nchunk = L.lib().sca_coord_map_bwd_chunks(rows)
         part = [kp.new_empty(2 * nchunk * N * idx[g].numel()) for g in range(G)]
@@ -934,12 +989,14 @@ class CoordinateMappingOp(Function):
                                      Wy[g].data_ptr(), dxe[g].data_ptr(), dye[g].data_ptr(), dwx[g].data_ptr(),
                                      dwy[g].data_ptr(), ptr(dkp), part[g].data_ptr()) for g in gs])
             L.check(L.lib().sca_coord_map_bwd(len(gs), arr, rows, K_all, N, L.stream_handle()), "sca_coord_map_bwd")
-        dbx = [kp.new_empty(N) if ctx.has_b[g] else None for g in range(G)]
-        dby = [kp.new_empty(N) if ctx.has_b[g] else None for g in range(G)]
+        params_produced(list(Wx) + list(Wy))
+        dbx = [param_grad_empty(b) if b is not None else None for b in ctx.bx]
+        dby = [param_grad_empty(b) if b is not None else None for b in ctx.by]
         pairs = [(dxe[g], dbx[g], 1.0) for g in range(G) if dbx[g] is not None] + \
                 [(dye[g], dby[g], 1.0) for g in range(G) if dby[g] is not None]
         if pairs:
             reduce_rows(pairs, rows, 1, N, N, 0)
+            params_produced(list(ctx.bx) + list(ctx.by))
         return (None, dkp) + (None,) * G + tuple(dwx) + tuple(dbx) + tuple(dwy) + tuple(dby)
 
 
@@ -977,7 +1034,7 @@ class LinearGelu(Function):
             ys.append(y)
             zs.append(z)
         gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.has_r, ctx.has_b = G, has_r, [bb is not None for bb in b]
+        ctx.G, ctx.has_r, ctx.b = G, has_r, tuple(b)  # biases: parameters (leaves) or None
         ctx.save_for_backward(*x, *W, *zs)
         return tuple(ys)
 
@@ -996,7 +1053,7 @@ class LinearGelu(Function):
             probs.append(_prob([_seg(dz[g], W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
             dxs.append(dx)
         gemm(L.GEMM_NN, probs)
-        wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.has_b[g]) for g in range(G)])
+        wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
         return (None, None) + tuple(dxs) + tuple(w for w, _ in wg) + tuple(bb for _, bb in wg) + \
             (tuple(dys) if ctx.has_r else ())
 

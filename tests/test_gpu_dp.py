@@ -1,0 +1,135 @@
+"""Data parallelism on the HIP path (BASELINE config 4), in one process.
+
+* Batch additivity: the config-2 model (4 streams, d 256, L 4) on two 8-clip halves through
+  the HIP kernels — the sum of the halves' gradients equals the full 16-clip HIP gradient
+  and the CPU oracle's, within the north-star 1e-3.  This is exactly what the all-reduce of
+  an 8-GPU x 8-clip run relies on (config 4: B = 64 = 8 x 8).
+* The bucketed reducer (scattennet_amd.dp.GradBuckets) at world size 1 over RCCL, with the
+  collectives forced on (SCA_DP_FORCE): discovery step, eager bucketed step, then the step
+  captured into a hipGraph WITH the bucket all-reduces and replayed — gradients identical to
+  the plain (no-DP) HIP gradients, `.grad` views of the flat buckets.
+"""
+import os
+
+import pytest
+import torch
+
+from oracle import sca_oracle as O
+from tests.golden_util import close, rel_err
+
+PARITY_TOL = 1e-3
+
+
+def _cfg2(B):
+    from scattennet_amd import workloads as W
+    return dict(W.WORKLOADS["cfg2"], B=B)
+
+
+def _grads(model, kp, mask, gout):
+    for p in model.parameters():
+        p.grad = None
+    outs = model(kp, mask)
+    torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+    torch.cuda.synchronize()
+    return {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.gpu
+def test_half_batch_gradients_sum_to_full_batch():
+    from scattennet_amd import workloads as W
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    w16 = _cfg2(16)
+    model = W.build_streams(w16, dev, seed=4, init="random")
+    kp, mask, gout = W.synthetic_batch(w16, dev, seed=9, ragged=False)
+    g = torch.Generator().manual_seed(21)
+    lens = torch.randint(1, w16["T"] + 1, (16,), generator=g)
+    lens[3], lens[11] = w16["T"], 1
+    mask = (torch.arange(w16["T"])[None] < lens[:, None]).long().to(dev)
+    full = _grads(model, kp, mask, gout)
+    h0 = _grads(model, kp[:8], mask[:8], gout[:, :8].contiguous())
+    h1 = _grads(model, kp[8:], mask[8:], gout[:, 8:].contiguous())
+    assert set(full) == set(h0) == set(h1)
+    gscale = max(float(v.abs().max()) for v in full.values())
+    for k in full:
+        s = h0[k] + h1[k]
+        assert close(s.cpu(), full[k].cpu(), PARITY_TOL, gscale), (k, rel_err(s, full[k]))
+
+    # ... and the oracle's full-batch gradient (every stream, every parameter)
+    cfg = W.model_cfg(w16["d"], w16["H"], w16["L"], maxpos=w16["maxpos"])
+    groups = W.split_groups(w16["groups"])
+    plist = [{k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+             for m in model.streams]
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    outs = O.multi_stream_sca(plist, kp.cpu(), mask.cpu(), groups, cfg)
+    torch.autograd.backward(outs, [gout[i].cpu() for i in range(len(outs))])
+    ref = {f"streams.{s}.{k}": v.grad for s, p in enumerate(plist) for k, v in p.items() if v.grad is not None}
+    rscale = max(float(v.abs().max()) for v in ref.values())
+    for k, v in ref.items():
+        s = (h0[k] + h1[k]).cpu()
+        assert close(s, v, PARITY_TOL, rscale), (k, rel_err(s, v))
+
+
+@pytest.mark.gpu
+def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
+    import torch.distributed as dist
+
+    from scattennet_amd import ops, workloads as W
+    from scattennet_amd.dp import GradBuckets
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    w = dict(W.WORKLOADS["cfg2"], B=4, T=128)
+    model = W.build_streams(w, dev, seed=2, init="random")
+    kp, mask, gout = W.synthetic_batch(w, dev, seed=3, ragged=True)
+    ref = _grads(model, kp, mask, gout)  # plain HIP gradients, no sink
+
+    monkeypatch.setenv("SCA_DP_FORCE", "1")
+    init_here = not dist.is_initialized()
+    if init_here:
+        port = 29400 + os.getpid() % 500
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=dev)
+    red = GradBuckets(model.parameters(), bucket_mb=6)
+    try:
+        assert red.collective and red.overlap
+        params = list(model.parameters())
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # discovery step, then a bucketed eager step
+                for p in params:
+                    p.grad = None
+                outs = model(kp, mask)
+                torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        assert len(red.plan) >= 2
+        eager = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+        for p in params:
+            p.grad = None
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # RCCL watchdog thread
+            outs = model(kp, mask)
+            torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+        for p in params:  # poison the buckets: the replay must rewrite every planned gradient
+            if p.grad is not None:
+                p.grad.fill_(float("nan"))
+        graph.replay()
+        graph.replay()
+        torch.cuda.synchronize()
+        replay = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+        flat0 = red.flat.data_ptr()
+        views = [p.grad.data_ptr() - flat0 for i, p in enumerate(params) if i in red.slot]
+        assert all(0 <= v < red.flat.numel() * 4 for v in views)
+        assert set(ref) == set(eager) == set(replay)
+        for k in ref:
+            assert torch.equal(eager[k], ref[k]), k
+            assert torch.equal(replay[k], ref[k]), k
+        assert red.last_fallback == []
+    finally:
+        red.close()
+        ops.set_grad_sink(None)
+        if init_here:
+            dist.destroy_process_group()

@@ -78,12 +78,36 @@ def test_bad_lengths_raise_like_torch():
     from scattennet_amd import heads
     x = torch.zeros(2, 8, 5)
     with pytest.raises(RuntimeError, match="input_lengths"):
-        heads._validate_ctc(torch.ones(2, 3, dtype=torch.long), torch.tensor([3, 2]), torch.tensor([9, 8]), 8, 5)
+        heads._validate_ctc(torch.ones(2, 3, dtype=torch.long), torch.tensor([3, 2]), torch.tensor([9, 8]), 2, 8, 5)
     with pytest.raises(RuntimeError, match="targets"):
-        heads._validate_ctc(torch.ones(2, 3, dtype=torch.long), torch.tensor([4, 2]), torch.tensor([8, 8]), 8, 5)
+        heads._validate_ctc(torch.ones(2, 3, dtype=torch.long), torch.tensor([4, 2]), torch.tensor([8, 8]), 2, 8, 5)
     with pytest.raises(RuntimeError, match="target values"):
         heads._validate_ctc(torch.full((2, 3), 5, dtype=torch.long), torch.tensor([3, 2]), torch.tensor([8, 8]),
-                            8, x.shape[-1])
+                            2, 8, x.shape[-1])
+
+
+def test_batch_size_mismatches_raise():
+    """labels / input_lengths / target_lengths must hold one entry per clip (the kernels index
+    them by clip); the CPU-side checks run before any launch."""
+    from scattennet_amd import heads
+    x = torch.zeros(3, 8, 5)  # a CPU tensor: the checks must fire before the device check
+    with pytest.raises(RuntimeError, match="labels must be"):
+        heads.compute_loss(torch.ones(2, 3, dtype=torch.long), torch.tensor([3, 2, 1]), x, torch.tensor([8, 8, 8]))
+    with pytest.raises(RuntimeError, match="target_lengths"):
+        heads.compute_loss(torch.ones(3, 3, dtype=torch.long), torch.tensor([3, 2]), x, torch.tensor([8, 8, 8]))
+    with pytest.raises(RuntimeError, match="input_lengths"):
+        heads.compute_loss(torch.ones(3, 3, dtype=torch.long), torch.tensor([3, 2, 1]), x, torch.tensor([8, 8]))
+
+
+def test_concatenated_targets_are_split_by_lengths():
+    """nn.CTCLoss's 1-D target form: clip b's labels are the next tgt_len[b] entries (lengths
+    clamped to >= 1 first, as the reference passes them)."""
+    from scattennet_amd import heads
+    flat = torch.tensor([4, 1, 2, 3, 3, 2])
+    out = heads._pad_concatenated(flat, torch.tensor([2, 0, 3]), 3)
+    assert out.tolist() == [[4, 1, 0], [2, 0, 0], [3, 3, 2]]
+    with pytest.raises(RuntimeError, match="sum to"):
+        heads._pad_concatenated(flat[:4], torch.tensor([2, 0, 3]), 3)
 
 
 # ---------------------------------------------------------------------------- GPU parity
@@ -107,8 +131,9 @@ def test_hip_ctc_matches_reference(path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("concat", [False, True])
 @pytest.mark.parametrize("B,T,C,S", [(8, 64, 1124, 24), (3, 200, 64, 90), (16, 1, 8, 1)])
-def test_hip_ctc_matches_oracle(B, T, C, S):
+def test_hip_ctc_matches_oracle(B, T, C, S, concat):
     rng = np.random.default_rng(B * 1000 + T)
     x = (rng.standard_normal((B, T, C)) * 2).astype(np.float32)
     labels = rng.integers(1, C, size=(B, S)).astype(np.int32)
@@ -122,6 +147,8 @@ def test_hip_ctc_matches_oracle(B, T, C, S):
             x[b, t, labels[b, min(t * Sb // Tb, Sb - 1)]] += 8.0
     f = {"logits": x, "labels": labels, "in_len": in_len.astype(np.int32), "tgt_len": tgt_len.astype(np.int32)}
     ref_loss, ref_nll, ref_dx = O.ctc_compute_loss(x, labels, in_len, tgt_len)
+    if concat:  # the same targets in nn.CTCLoss's concatenated 1-D form
+        f["labels"] = np.concatenate([labels[b, :max(int(tgt_len[b]), 1)] for b in range(B)])
     loss, nll, dx = _hip_ctc(f)
     np.testing.assert_allclose(nll, ref_nll, rtol=1e-5, atol=2e-4)
     np.testing.assert_allclose(loss, ref_loss, **LOSS_TOL)

@@ -1,0 +1,108 @@
+"""Attention-mask contract at the drop-in boundary (model/attention.py:65/117/171:
+`attn_weights += attention_mask`).
+
+Every additive mask the reference accepts — anything broadcastable to (B, 1, Tq, Tk) — is
+expanded to the kernels' dense (B, Tq, Tk) layout before a launch; shapes the reference would
+reject (or that the kernels cannot take: per-head masks) raise; `None` raises TypeError as
+`attn_weights += None` does.  CPU tests cover the host-side resolution; the GPU test runs the
+four broadcast shapes through the HIP kernels against the oracle.
+"""
+import pytest
+import torch
+
+from oracle import sca_oracle as O
+from tests.golden_util import close, rel_err
+
+PARITY_TOL = 1e-3
+
+
+def _resolve(mask, causal=False, B=3, Tq=5, Tk=7):
+    from scattennet_amd.attention import _resolve_mask
+    return _resolve_mask(mask, causal, B, Tq, Tk, torch.device("cpu"))
+
+
+@pytest.mark.parametrize("shape", [(3, 1, 5, 7), (1, 1, 5, 7), (3, 1, 1, 7), (5, 7), (7,), (1, 5, 1), ()])
+def test_broadcast_masks_expand_to_dense(shape):
+    m = torch.randn(shape)
+    kv, am, plus = _resolve(m)
+    assert kv is None and not plus
+    assert am.shape == (3, 5, 7) and am.is_contiguous() and am.dtype == torch.float32
+    want = m.reshape((1,) * (4 - m.dim()) + tuple(m.shape)).expand(3, 1, 5, 7)[:, 0]
+    assert torch.equal(am, want)
+
+
+@pytest.mark.parametrize("shape", [(3, 2, 5, 7), (2, 1, 5, 7), (3, 1, 4, 7), (5, 6), (1, 3, 1, 5, 7)])
+def test_non_broadcastable_masks_raise(shape):
+    with pytest.raises(ValueError):
+        _resolve(torch.zeros(shape))
+
+
+def test_none_mask_raises_type_error():
+    with pytest.raises(TypeError):
+        _resolve(None)
+
+
+def test_key_padding_mask_shape_checked():
+    from scattennet_amd.utils import key_padding_mask
+    kv, am, plus = _resolve(key_padding_mask(torch.ones(3, 7, dtype=torch.long), causal=True), causal=True)
+    assert kv.shape == (3, 7) and am is None and plus
+    with pytest.raises(ValueError):
+        _resolve(key_padding_mask(torch.ones(2, 7, dtype=torch.long)))
+
+
+def test_bool_and_int_masks_add_like_the_reference():
+    m = torch.tensor([[True, False, True, True, False, True, True]])
+    _, am, _ = _resolve(m)
+    assert torch.equal(am[0, 0], m[0].float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["self", "causal", "cross"])
+@pytest.mark.parametrize("form", ["B1TT", "11TT", "B11T", "TT"])
+def test_gpu_broadcast_masks_vs_oracle(kind, form):
+    import scattennet_amd as S
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    B, Tq, d, H = 3, 48, 64, 4
+    Tk = 40 if kind == "cross" else Tq
+    torch.manual_seed(17 * len(kind) + len(form))
+    cls = {"self": S.SelfAttention, "causal": S.SelfCausalAttention, "cross": S.CrossAttention}[kind]
+    m = cls(d, H)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn_like(p) / (p.shape[-1] ** 0.5 if p.dim() == 2 else 10.0))
+    m = m.to(dev)
+    shape = {"B1TT": (B, 1, Tq, Tk), "11TT": (1, 1, Tq, Tk), "B11T": (B, 1, 1, Tk), "TT": (Tq, Tk)}[form]
+    # additive masks in the reference's vocabulary: finfo.min on dropped keys, small offsets elsewhere
+    am = torch.randn(shape) * 0.5
+    drop = torch.rand(shape) < 0.3
+    am = am.masked_fill(drop, O.FMIN)
+    x, kv = torch.randn(B, Tq, d), torch.randn(B, Tk, d)
+    xg, kvg = x.to(dev).requires_grad_(True), kv.to(dev).requires_grad_(True)
+    out = m(xg, kvg, am.to(dev)) if kind == "cross" else m(xg, am.to(dev))
+    gout = torch.randn(out.shape)
+    out.backward(gout.to(dev))
+
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    xr, kvr = x.clone().requires_grad_(True), kv.clone().requires_grad_(True)
+    ref = O.attention({"a." + k: v for k, v in p.items()}, "a", xr, kvr if kind == "cross" else xr, am, H, kind)
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * gout).sum().backward()
+    assert rel_err(xg.grad, xr.grad) < PARITY_TOL
+    if kind == "cross":
+        assert rel_err(kvg.grad, kvr.grad) < PARITY_TOL
+    gscale = max(float(v.grad.abs().max()) for v in p.values())
+    named = dict(m.named_parameters())
+    for k, v in p.items():
+        assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))
+
+
+@pytest.mark.gpu
+def test_gpu_none_mask_raises():
+    import scattennet_amd as S
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    m = S.SelfAttention(64, 4).cuda()
+    with pytest.raises(TypeError):
+        m(torch.randn(2, 8, 64, device="cuda"), None)

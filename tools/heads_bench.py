@@ -3,7 +3,9 @@
 Workload: MSCA_Net's head at the 2014T yaml shapes — left/right/body features (B, T/4, 512),
 fused features (B, T/4, 1024), vocabulary C, BiLSTM alignment head (1024 -> 2 x 512, 2
 layers), two CTC losses (alignment + fuse_coord) and three SeqKD distillation terms
-(model/__init__.py:119-236), forward + backward.  Synthetic data; heads in eval mode.
+(model/__init__.py:119-236).  As in the reference's training step, the alignment head and its
+CTC loss run forward only: `total_loss` sums the fuse_coord CTC loss and the three SeqKD terms
+(model/__init__.py:207,236), so backward never reaches the BiLSTM.  Synthetic data; eval mode.
 Prints one JSON line with ms per step and the per-part split.
 
 Usage: python tools/heads_bench.py [--B 8] [--T 64] [--C 1124] [--steps 20]
@@ -48,8 +50,9 @@ def main():
         ev[0].record()
         out = head(feats[0], feats[1], fuse, feats[2])
         ev[1].record()
-        loss = heads.compute_loss(labels, tl, out["alignment_gloss_logits"], il)
-        loss = loss + heads.compute_loss(labels, tl, out["fuse_coord_gloss_logits"], il)
+        # alignment_loss is computed and reported by the reference but not added to total_loss
+        heads.compute_loss(labels, tl, out["alignment_gloss_logits"], il)
+        loss = heads.compute_loss(labels, tl, out["fuse_coord_gloss_logits"], il)
         for k, w in weights.items():
             loss = loss + heads.distillation_loss(out[k], out["fuse_coord_gloss_logits"], w)
         ev[2].record()
@@ -70,7 +73,7 @@ def main():
     fwd = sum(e[0].elapsed_time(e[1]) for e in parts) / a.steps
     loss_ms = sum(e[1].elapsed_time(e[2]) for e in parts) / a.steps
     bwd = sum(e[2].elapsed_time(e[3]) for e in parts) / a.steps
-    print(json.dumps({"workload": "recognition heads + CTC x2 + SeqKD x3, fwd+bwd", "B": B, "T": T, "C": a.C,
+    print(json.dumps({"workload": "recognition heads + CTC x2 + SeqKD x3 fwd; bwd of total_loss (fuse CTC + SeqKD x3)", "B": B, "T": T, "C": a.C,
                       "ms_per_step": round(ms, 3), "head_fwd_ms": round(fwd, 3), "losses_fwd_ms": round(loss_ms, 3),
                       "bwd_ms": round(bwd, 3), "clips_per_s": round(B / ms * 1e3, 1)}))
 
