@@ -135,6 +135,33 @@ typedef struct {
 int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                 void* stream);
 
+/* NN input-gradient GEMM + the backward of the LayerNorm that produced its input, in one
+ * launch (d_model = 256).  Per problem:
+ *   C  = resid + sum_s alpha * A_s B_s           (sca_gemm NN, epilogue: resid only)
+ *      = dL/dy, the gradient w.r.t. the output y of an nn.LayerNorm whose input was x
+ *   dx = rstd * (C*gamma - mean_n(C*gamma) - xhat * mean_n(C*gamma*xhat)),
+ *        xhat = (x - mean) * rstd                  (aten native_layer_norm_backward)
+ *   partial[0][blk][n] = sum_{rows of blk} C * xhat,  partial[1][blk][n] = sum C
+ *        (fixed-order dgamma / dbeta partials per 32-row block; blk = row / 32, reduce
+ *        them with sca_reduce_rows over nblk = sca_gemm_lnb_blocks(M) rows)
+ * Replaces the input-gradient GEMM of a post-LN block's first op (the attention block's
+ * dX = dq Wq + dk Wk + dv Wv + dY, the FFN's dx = dz W1 + dY) followed by the separate
+ * LayerNorm backward of the block below (keypoint_module.py:69-72, 105-109).
+ * Requires N == 256, 1..3 segments with K a positive multiple of 32 and one alpha, B
+ * k-major (B[k][n] at B + k*ldb + n), 16-byte aligned operands, leading dimensions
+ * multiples of 4; else SCA_ERR_ARG.                                                       */
+typedef struct {
+  const float* x;     /* [M, 256] LayerNorm input saved by the forward */
+  const float* mean;  /* [M] */
+  const float* rstd;  /* [M] */
+  const float* gamma; /* [256] */
+  float* dx;          /* [M, 256] gradient w.r.t. x */
+  float* partial;     /* [2, nblk, 256] dgamma / dbeta partials */
+} sca_gemm_lnb_problem;
+
+int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);
+int sca_gemm_lnb_blocks(int M);
+
 /* Tuning knob: force the workgroup tile of one layout (0 = built-in heuristic,
  * 1 = 64x64, 2 = 128x64, 3 = 64x128, 4 = 128x128).  Process-global; not thread-safe.   */
 int sca_gemm_tile_override(int layout, int tile);

@@ -68,6 +68,11 @@ class GemmLnProblem(ctypes.Structure):
     _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("y", c_void_p), ("mean", c_void_p), ("rstd", c_void_p)]
 
 
+class GemmLnbProblem(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("gamma", c_void_p), ("dx", c_void_p),
+                ("partial", c_void_p)]
+
+
 class PoolProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("dy", c_void_p), ("dx", c_void_p)]
 
@@ -105,6 +110,8 @@ EXPORTS = {
     "sca_gemm_reduce": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "sca_gemm_tile_override": ([c_int, c_int], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
+    "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "sca_gemm_lnb_blocks": ([c_int], c_int),
     "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
     "sca_attn_bwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
     "sca_attn_bwd_fused": ([c_int], c_int),

@@ -731,6 +731,165 @@ __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
   }
 }
 
+// ------------------------------------------------------------------------------ GEMM + LayerNorm backward
+// NN input-gradient GEMM whose epilogue runs the backward of the LayerNorm below it (the
+// post-LN block boundary, keypoint_module.py:69-72 / 105-109, walked backwards): a workgroup
+// owns 32 FULL rows (32 x 256), so C = dL/dy is complete in the workgroup and the row
+// reductions of the LayerNorm backward never leave it; the separate ln_bwd launch and its
+// re-read of dL/dy disappear.  Main loop: the LDS-DMA ring of gemm_ln_kernel with a k-major
+// B image (one 1-KiB DMA piece per k-row, rows 1056 B apart so the two half-waves of a
+// fragment read, 4 k-rows apart, land on different banks); segments (dq Wq + dk Wk + dv Wv)
+// are one continuous slice sequence.  Epilogue: the tile goes through LDS; each wave takes 4
+// rows (float4 lanes, interleaved shuffle reductions); dgamma / dbeta partials are summed
+// over the 32 rows in fixed order (waves through LDS) into one partial row per block.
+// 8 waves (512 threads, two per SIMD, each a 32x32 column block): with one workgroup per CU
+// (113 KB of LDS) a second wave per SIMD hides the DMA waits and the barrier; 4 waves of
+// 32x64 ran 45 us per 4 x (2048 x 256 x 768) launch.
+constexpr int LB_BM = 32, LB_S = 3;
+constexpr int LB_BROW = 1056;                        // bytes per k-row of the B image
+constexpr int LB_A_BYTES = LB_BM * GL_BK * 4;        // 4 KiB
+constexpr int LB_STAGE = LB_A_BYTES + GL_BK * LB_BROW;
+constexpr int LB_RED_OFF = 40 * 1024;                // epilogue: V tile at 0, wave partials here
+
+struct GemmLnbArgs {
+  sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
+  sca_gemm_lnb_problem ln[SCA_GEMM_MAX_PROBLEMS];
+};
+
+__global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
+  __shared__ __attribute__((aligned(1024))) char smem[LB_S * LB_STAGE];
+  static_assert(LB_RED_OFF >= LB_BM * LG_VS * 4 && LB_RED_OFF + 2 * 8 * LG_BN * 4 <= LB_S * LB_STAGE, "LDS map");
+  const unsigned gx = gridDim.x;
+  const unsigned nwg = gx * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * blockIdx.z;
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int pid = wgid / gx, bx = wgid % gx;
+  const sca_gemm_problem& P = args.p[pid];
+  const sca_gemm_lnb_problem& LN = args.ln[pid];
+  const int m0 = bx * LB_BM;
+  if (m0 >= P.M) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;  // 8 waves: 2 per SIMD
+  const bool has_a = wave < 4;                                  // waves 0-3 also fetch an A piece
+
+  int seg_n[SCA_GEMM_MAX_SEGS];
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
+    seg_n[s] = s < P.nseg ? P.seg[s].K / GL_BK : 0;
+    total += seg_n[s];
+  }
+  // issue state: A piece `wave` (rows 8*wave ..) and B pieces = k-rows 4*wave .. 4*wave+3
+  int iseg = -1, tseg0 = 0, tend = 0;
+  const float* pa = nullptr;
+  const float* pb = nullptr;
+  long ldb = 0;
+  auto dma = [&](int t, int stage) {
+    while (t >= tend) {
+      ++iseg;
+      tseg0 = tend;
+      tend += seg_n[iseg];
+      const sca_gemm_seg& G = P.seg[iseg];
+      pa = lg_src(G.A, G.lda, m0, P.M, has_a ? wave : 0, lane);
+      ldb = G.ldb;
+      pb = G.B + (long)(4 * wave) * ldb + 4 * lane;
+    }
+    const long k0 = (long)(t - tseg0) * GL_BK;
+    char* base = smem + stage * LB_STAGE;
+    if (has_a) gl_dma(pa + k0, base + wave * GL_PIECE);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) gl_dma(pb + (k0 + c) * ldb, base + LB_A_BYTES + (4 * wave + c) * LB_BROW);
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int col = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < LB_S - 1; ++i)
+    if (i < total) dma(i, i);
+  for (int t = 0; t < total; ++t) {
+    if (t + LB_S - 2 < total) {
+      if (has_a) gl_wait_vm<5 * (LB_S - 2)>();
+      else gl_wait_vm<4 * (LB_S - 2)>();
+    } else {
+      gl_wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + LB_S - 1 < total) dma(t + LB_S - 1, (t + LB_S - 1) % LB_S);
+    const char* As = smem + (t % LB_S) * LB_STAGE;
+    const float* Bf = reinterpret_cast<const float*>(As + LB_A_BYTES);
+    f32x4 fa[4], fb[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      fa[g] = gl_frag<true>(As, 0, g, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[g][j] = Bf[(8 * g + 4 * h + j) * (LB_BROW / 4) + 32 * wave + col];
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
+  }
+  // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
+  __syncthreads();
+  float* V = reinterpret_cast<float*>(smem);
+  const float alpha = P.seg[0].alpha;
+  const int rowh = 4 * h;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
+  __syncthreads();
+
+  constexpr int RPW = LB_BM / 8;
+  const int n = 4 * lane;
+  const f32x4 gam = ld4(LN.gamma + n);
+  const float invN = 1.0f / LG_BN;
+  f32x4 g[RPW], xh[RPW];
+  float s1[RPW], s2[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = min(m0 + RPW * wave + i, P.M - 1);
+    g[i] = ld4(&V[(RPW * wave + i) * LG_VS + n]);
+    if (P.resid) g[i] += ld4(P.resid + (long)m * P.ldr + n);
+    xh[i] = (ld4(LN.x + (long)m * LG_BN + n) - LN.mean[m]) * LN.rstd[m];
+    const f32x4 gg = g[i] * gam;
+    s1[i] = (gg[0] + gg[1]) + (gg[2] + gg[3]);
+    const f32x4 ggx = gg * xh[i];
+    s2[i] = (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      s1[i] += __shfl_xor(s1[i], o, 64);
+      s2[i] += __shfl_xor(s2[i], o, 64);
+    }
+  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pbsum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = m0 + RPW * wave + i;
+    if (m < P.M) {
+      const float rstd = LN.rstd[m];
+      st4(P.C + (long)m * P.ldc + n, g[i]);
+      st4(LN.dx + (long)m * LG_BN + n, (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rstd);
+      pg += g[i] * xh[i];
+      pbsum += g[i];
+    }
+  }
+  // the 8 waves' partial rows, summed in fixed order: threads 0-255 dgamma, 256-511 dbeta
+  float* red = reinterpret_cast<float*>(smem + LB_RED_OFF);
+  st4(red + wave * LG_BN + n, pg);
+  st4(red + (8 + wave) * LG_BN + n, pbsum);
+  __syncthreads();
+  const int c = threadIdx.x & (LG_BN - 1), which = threadIdx.x >> 8;
+  const float* rr = red + which * 8 * LG_BN + c;
+  const float sum = (((rr[0] + rr[LG_BN]) + (rr[2 * LG_BN] + rr[3 * LG_BN])) +
+                     ((rr[4 * LG_BN] + rr[5 * LG_BN]) + (rr[6 * LG_BN] + rr[7 * LG_BN])));
+  const long nblk = (P.M + LB_BM - 1) / LB_BM;
+  LN.partial[(which * nblk + bx) * LG_BN + c] = sum;
+}
+
 // ------------------------------------------------------------------------------ persistent
 // One output tile of the persistent kernel: integers only (wave-uniform).  Pointers and
 // leading dimensions are re-read from the kernel arguments (scalar loads) at each fetch,
@@ -1219,5 +1378,49 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
     hipLaunchKernelGGL(gemm_ln_kernel<GL_A32>, dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
   }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_gemm_lnb_blocks(int M) { return M > 0 ? (M + LB_BM - 1) / LB_BM : 0; }
+
+extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb,
+                            void* stream) {
+  if (nprob <= 0) return SCA_OK;
+  if (nprob > SCA_GEMM_MAX_PROBLEMS || !probs || !lnb) {
+    sca_set_error("sca_gemm_lnb: bad nprob / pointers");
+    return SCA_ERR_ARG;
+  }
+  GemmLnbArgs a;
+  int maxM = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const sca_gemm_problem& P = probs[i];
+    const sca_gemm_lnb_problem& L = lnb[i];
+    bool ok = P.nseg >= 1 && P.nseg <= SCA_GEMM_MAX_SEGS && P.N == LG_BN && P.M >= 0 && P.C && L.x && L.mean &&
+              L.rstd && L.gamma && L.dx && L.partial && P.epi == 0 && !P.bias && !P.bias_grad &&
+              P.post_scale == 1.f && (P.ldc & 3) == 0 && P.ldc >= LG_BN &&
+              (!P.resid || ((P.ldr & 3) == 0 && P.ldr >= LG_BN));
+    uintptr_t al = reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
+                   reinterpret_cast<uintptr_t>(L.x) | reinterpret_cast<uintptr_t>(L.gamma) |
+                   reinterpret_cast<uintptr_t>(L.dx);
+    for (int s = 0; ok && s < P.nseg; ++s) {
+      const sca_gemm_seg& S = P.seg[s];
+      ok = S.A && S.B && S.K >= GL_BK && S.K % GL_BK == 0 && (S.lda & 3) == 0 && S.lda >= S.K &&
+           (S.ldb & 3) == 0 && S.ldb >= LG_BN && S.alpha == P.seg[0].alpha;
+      al |= reinterpret_cast<uintptr_t>(S.A) | reinterpret_cast<uintptr_t>(S.B);
+    }
+    if (!ok || (al & 15)) {
+      sca_set_error("sca_gemm_lnb: needs N == 256, 1-3 segments with K a positive multiple of 32 and one alpha, "
+                    "k-major B, no epilogue other than resid, 16-byte aligned operands with leading dimensions "
+                    "multiple of 4");
+      return SCA_ERR_ARG;
+    }
+    a.p[i] = P;
+    a.ln[i] = L;
+    maxM = maxM > P.M ? maxM : P.M;
+  }
+  if (maxM == 0) return SCA_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(gemm_lnb_kernel, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

@@ -215,6 +215,99 @@ def gemm_ln(probs, lns, eps):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
+_FUSE_LNB = __import__("os").environ.get("SCA_FUSE_LNB", "1") != "0"
+
+
+class LnSaved:
+    """What a fused GEMM + post-LN LayerNorm forward (sca_gemm_ln) leaves on its output
+    tensor (`y._sca_ln`) so that the op consuming y can run this LayerNorm's backward in
+    its own input-gradient GEMM's epilogue (sca_gemm_lnb): the LN input v, its row mean /
+    rstd and gamma.  `handoff` carries the result back to the producer's backward:
+    (dL/dy as the consumer returned it, its version, dL/dv, dgamma/dbeta partials, nblk)."""
+    __slots__ = ("v", "mean", "rstd", "gamma", "handoff")
+
+    def __init__(self, v, mean, rstd, gamma):
+        self.v, self.mean, self.rstd, self.gamma, self.handoff = v, mean, rstd, gamma, None
+
+
+def ln_saved_of(ts):
+    """Consumer forward: the LnSaved of each input (all G or None)."""
+    if not _FUSE_LNB:
+        return None
+    out = [getattr(t, "_sca_ln", None) for t in ts]
+    return out if all(o is not None for o in out) else None
+
+
+def _attach_ln_saved(ys, vs, means, rstds, gam):
+    objs = [LnSaved(vs[g], means[g], rstds[g], gam[g]) for g in range(len(ys))]
+    for y, o in zip(ys, objs):
+        y._sca_ln = o
+    return objs
+
+
+def gemm_lnb(probs, lnp):
+    """Consumer backward: the NN input-gradient GEMMs `probs` (C = dL/dy of the LayerNorms
+    `lnp`, N = 256) with those LayerNorms' backward fused (sca_gemm_lnb); the LN-input
+    gradients and dgamma/dbeta partials are handed to the producers' backward."""
+    lib = L.lib()
+    M = probs[0].M
+    nblk = lib.sca_gemm_lnb_blocks(M)
+    dv = [torch.empty_like(o.v) for o in lnp]
+    part = [o.v.new_empty(2 * nblk * o.v.shape[-1]) for o in lnp]
+    arr = (L.GemmProblem * len(probs))(*probs)
+    larr = (L.GemmLnbProblem * len(lnp))(*[L.GemmLnbProblem(o.v.data_ptr(), o.mean.data_ptr(), o.rstd.data_ptr(),
+                                                           o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr())
+                                            for g, o in enumerate(lnp)])
+    flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
+    with _timed("gemm_lnb_kernel", flops):
+        L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
+    return dv, part, nblk
+
+
+def hand_off(lnp, dxs, dv, part, nblk):
+    for g, o in enumerate(lnp):
+        o.handoff = (dxs[g], dxs[g]._version, dv[g], part[g], nblk)
+
+
+def _take_handoff(lnsaved, dys):
+    """Producer backward: the consumer's precomputed LayerNorm backward, valid only if the
+    incoming gradients ARE the tensors the consumer returned, untouched (the consumer was
+    the output's only one: with another, autograd's sum is a new tensor)."""
+    if lnsaved is None:
+        return None
+    hs = [o.handoff for o in lnsaved]
+    for o in lnsaved:
+        o.handoff = None
+    for h, d in zip(hs, dys):
+        if h is None or d is None or d.data_ptr() != h[0].data_ptr() or d._version != h[1] or d.shape != h[0].shape:
+            return None
+    return hs
+
+
+def _ln_bwd_or_handoff(dys, vs, gam, means, rstds, lnsaved, bet):
+    """The fused post-LN LayerNorm's backward: taken over from the consumer's sca_gemm_lnb
+    when it ran, else ln_bwd.  -> (dL/dv, dgamma, dbeta, deferred affine finish)."""
+    hs = _take_handoff(lnsaved, dys)
+    params = tuple(gam) + tuple(bet)
+    if hs is None:
+        dys = _contig(_zeros_for_none(dys, vs))
+        return _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE, params=params)
+    G, N, nblk = len(gam), gam[0].shape[0], hs[0][4]
+    dg = [param_grad_empty(t) for t in gam]
+    db = [param_grad_empty(b) for b in bet]
+    part = [h[3] for h in hs]
+
+    def reduce():
+        reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
+                    [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0)
+    finish = (reduce, part, params)
+    if not _LN_AFFINE_SIDE:
+        reduce()
+        params_produced(params)
+        finish = None
+    return [h[2] for h in hs], dg, db, finish
+
+
 def _ln_fwd_outputs(xs):
     """(v, y, mean, rstd) buffers of a fused GEMM + LayerNorm over the rows of xs."""
     rows = xs[0].numel() // xs[0].shape[-1]
@@ -566,6 +659,7 @@ class AttentionBlock(Function):
         if ln:
             gam, bet, ts = ts[-2 * G:-G], ts[-G:], ts[:-2 * G]
         causal = kind == "causal"
+        lnprev = ln_saved_of(ts[:G])  # the query input came out of a fused GEMM + LayerNorm
         xq = _contig(ts[:G])
         o_ = G
         xkv = _contig(ts[o_:o_ + G]) if cross else xq
@@ -606,6 +700,8 @@ class AttentionBlock(Function):
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
+        ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam) if ln else None
+        ctx.lnprev = lnprev if (lnprev is not None and d == 256 and has_resid) else None
         ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
                               *sm, *sl, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
@@ -629,15 +725,15 @@ class AttentionBlock(Function):
         B, T, d = xq[0].shape
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
-        dys = _contig(_zeros_for_none(dys, xq))
         dgam = dbet = ()
         ln_finish = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             i += 6 * G
             vs, gam, means, rstds = (sv[i + j * G:i + (j + 1) * G] for j in range(4))
-            dys, dgam, dbet, ln_finish = _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE,
-                                                 params=tuple(gam) + ctx.bet)
+            dys, dgam, dbet, ln_finish = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
+        else:
+            dys = _contig(_zeros_for_none(dys, xq))
         dyo = dys  # gradient of the out-projection output: the dropout mask applied to dY
         if ctx.drop_p > 0:
             dyo = [torch.empty_like(t) for t in dys]
@@ -649,8 +745,9 @@ class AttentionBlock(Function):
         # runs with unit segment scales: dX = dq' Wq + dk Wk + dv' Wv, dWq = dq'^T x, ...
         dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do,
                                dq_scale=scale, dv_scale=av)
-        # input gradients (residual gradient fused as the epilogue's resid term)
-        dxq, dxkv, probs = [], [], []
+        # input gradients (residual gradient fused as the epilogue's resid term); with `lnprev`
+        # the query input's LayerNorm backward rides in the same launch (sca_gemm_lnb)
+        dxq, dxkv, probs, kvprobs = [], [], [], []
         for g in range(G):
             Wq, _, Wk, _, Wv, _ = W[6 * g:6 * g + 6]
             dqf, dkf, dvf = _flat(dq[g]), _flat(dk[g]), _flat(dv[g])
@@ -659,13 +756,18 @@ class AttentionBlock(Function):
             if cross:
                 gkv = torch.empty_like(xkv[g])
                 probs.append(_prob([_seg(dqf, Wq, d, d, d)], gx, B * T, d, d, resid=r, ldr=d))
-                probs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
+                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
                 dxkv.append(gkv)
             else:
                 probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
                                    gx, B * T, d, d, resid=r, ldr=d))
             dxq.append(gx)
-        gemm(L.GEMM_NN, probs)
+        if ctx.lnprev is not None:
+            hand_off(ctx.lnprev, dxq, *gemm_lnb(probs, ctx.lnprev))
+            ctx.lnprev = None
+            gemm(L.GEMM_NN, kvprobs)
+        else:
+            gemm(L.GEMM_NN, probs + kvprobs)
         # weight / bias gradients (bias colsum fused in the TN GEMMs)
         items = []
         for g in range(G):
@@ -737,6 +839,7 @@ class FeedForwardResidual(Function):
 
     @staticmethod
     def forward(ctx, G, has_r, drop_p, ln_eps, *ts):
+        lnprev = ln_saved_of(ts[:G])  # the input came out of a fused GEMM + LayerNorm
         x = _contig(ts[:G])
         W1, b1, W2, b2 = ts[G:2 * G], ts[2 * G:3 * G], ts[3 * G:4 * G], ts[4 * G:5 * G]
         ln = ln_eps is not None  # the block's last LayerNorm fused into fc2 (sca_gemm_ln)
@@ -768,6 +871,8 @@ class FeedForwardResidual(Function):
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
         ctx.b1, ctx.b2, ctx.bet = tuple(b1), tuple(b2), (tuple(bet) if ln else ())  # parameters (leaves)
+        ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam) if ln else None
+        ctx.lnprev = lnprev if (lnprev is not None and d == 256 and has_r and F_ % 32 == 0) else None
         ctx.save_for_backward(*x, *W1, *W2, *zs, *acts, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
 
@@ -776,14 +881,14 @@ class FeedForwardResidual(Function):
         G = ctx.G
         sv = ctx.saved_tensors
         x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
-        dys = _contig(_zeros_for_none(dys, x))
         dgam = dbet = ()
         ln_finish = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             vs, gam, means, rstds = (sv[(5 + i) * G:(6 + i) * G] for i in range(4))
-            dys, dgam, dbet, ln_finish = _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE,
-                                                 params=tuple(gam) + ctx.bet)
+            dys, dgam, dbet, ln_finish = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
+        else:
+            dys = _contig(_zeros_for_none(dys, x))
         B, T, d = x[0].shape
         M = B * T
         F_ = W1[0].shape[0]
@@ -796,10 +901,16 @@ class FeedForwardResidual(Function):
         # dz = mask1 * (dy' W2) * gelu'(z)
         gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
                                aux=zs[g], ldx=F_, drop=(ctx.s1[g], p) if p > 0 else None) for g in range(G)])
-        # dx = dz W1 + dy   (residual)
+        # dx = dz W1 + dy   (residual); with `lnprev` the input's LayerNorm backward rides in
+        # the same launch (sca_gemm_lnb)
         dx = [torch.empty_like(x[g]) for g in range(G)]
-        gemm(L.GEMM_NN, [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
-                               resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)])
+        probs = [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
+                       resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)]
+        if ctx.lnprev is not None:
+            hand_off(ctx.lnprev, dx, *gemm_lnb(probs, ctx.lnprev))
+            ctx.lnprev = None
+        else:
+            gemm(L.GEMM_NN, probs)
         items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], ctx.b2[g] if ctx.b2[g] is not None else True)
                  for g in range(G)] + \
                 [(dz[g], _flat(x[g]), 1.0, W1[g], ctx.b1[g] if ctx.b1[g] is not None else True) for g in range(G)]

@@ -41,7 +41,8 @@ _STRUCTS = {  # C struct in include/scatten.h -> ctypes mirror in scattennet_amd
     "sca_ln_bwd_problem": "LnBwdProblem", "sca_pool_problem": "PoolProblem", "sca_softmax_problem": "SoftmaxProblem",
     "sca_gelu_bwd_problem": "GeluBwdProblem", "sca_reduce_problem": "ReduceProblem",
     "sca_coord_map_problem": "CoordMapProblem", "sca_coord_map_bwd_problem": "CoordMapBwdProblem",
-    "sca_dropout_problem": "DropoutProblem",
+    "sca_dropout_problem": "DropoutProblem", "sca_gemm_ln_problem": "GemmLnProblem",
+    "sca_gemm_lnb_problem": "GemmLnbProblem",
 }
 
 

@@ -1,0 +1,134 @@
+"""GPU parity of the NN input-gradient GEMM + LayerNorm backward launch (sca_gemm_lnb).
+
+* the C ABI directly against a float64 restatement (C = resid + sum_s A_s B_s, then
+  aten's layer_norm backward of the LayerNorm whose output C is the gradient of), 1-3
+  segments, ragged M, the dgamma / dbeta partials summed;
+* the hand-off between post-LN blocks: two chained CoordinateAttention (self) blocks at
+  d_model 256 — the second block's input-gradient GEMM runs the first block's last
+  LayerNorm backward (and each block's FFN runs its attention LayerNorm backward) — against
+  the CPU oracle, forward and every gradient; and the same chain with a second consumer of
+  the first block's output, where the producer must NOT take the hand-off (autograd sums
+  the two consumers' gradients first).
+"""
+import pytest
+import torch
+
+from oracle import sca_oracle as O
+from tests.golden_util import close, rel_err
+
+PARITY_TOL = 1e-3
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+@pytest.mark.parametrize("M,Ks", [(2048, (768,)), (2048, (256, 256, 256)), (1000, (256,)), (33, (32, 64))])
+def test_gemm_lnb_c_abi_vs_float64(M, Ks):
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    torch.manual_seed(M + sum(Ks))
+    N = 256
+    segs, c64 = [], torch.zeros(M, N, dtype=torch.float64)
+    keep = []
+    for K in Ks:
+        A, B = torch.randn(M, K, device=dev), torch.randn(K, N, device=dev) / K ** 0.5
+        keep += [A, B]
+        segs.append(ops._seg(A, B, K, N, K))
+        c64 += A.double().cpu() @ B.double().cpu()
+    resid = torch.randn(M, N, device=dev)
+    c64 += resid.double().cpu()
+    x = torch.randn(M, N, device=dev) * 2 + 0.5
+    gam = torch.randn(N, device=dev)
+    mean = x.mean(-1)
+    rstd = 1.0 / (x.var(-1, unbiased=False) + 1e-5).sqrt()
+    C, dx = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    nblk = L.lib().sca_gemm_lnb_blocks(M)
+    part = torch.empty(2 * nblk * N, device=dev)
+    prob = ops._prob(segs, C, M, N, N, resid=resid, ldr=N)
+    lnp = L.GemmLnbProblem(x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gam.data_ptr(), dx.data_ptr(),
+                           part.data_ptr())
+    arr, larr = (L.GemmProblem * 1)(prob), (L.GemmLnbProblem * 1)(lnp)
+    L.check(L.lib().sca_gemm_lnb(1, arr, larr, L.stream_handle()), "sca_gemm_lnb")
+    torch.cuda.synchronize()
+    # float64 restatement of aten's layer_norm backward with dL/dy = C
+    x64 = x.double().cpu().requires_grad_(True)
+    g64, b64 = gam.double().cpu().requires_grad_(True), torch.zeros(N, dtype=torch.float64, requires_grad=True)
+    y64 = torch.nn.functional.layer_norm(x64, (N,), g64, b64, 1e-5)
+    y64.backward(c64)
+    assert rel_err(C.cpu(), c64) < 1e-5
+    assert rel_err(dx.cpu(), x64.grad) < 1e-4
+    pg = part[:nblk * N].view(nblk, N).sum(0).cpu()
+    pb = part[nblk * N:].view(nblk, N).sum(0).cpu()
+    assert rel_err(pg, g64.grad) < 1e-4
+    assert rel_err(pb, b64.grad) < 1e-4
+
+
+def test_gemm_lnb_rejects_bad_shapes():
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    A, B, C = torch.randn(64, 48, device=dev), torch.randn(48, 256, device=dev), torch.empty(64, 256, device=dev)
+    prob = ops._prob([ops._seg(A, B, 48, 256, 48)], C, 64, 256, 256)  # K = 48: not a multiple of 32
+    t = torch.empty(64, 256, device=dev)
+    lnp = L.GemmLnbProblem(t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr())
+    with pytest.raises(ValueError):
+        L.check(L.lib().sca_gemm_lnb(1, (L.GemmProblem * 1)(prob), (L.GemmLnbProblem * 1)(lnp),
+                                     L.stream_handle()), "sca_gemm_lnb")
+
+
+@pytest.mark.parametrize("second_consumer", [False, True])
+def test_chained_blocks_hand_off_layer_norm_backward(second_consumer):
+    _need_gpu()
+    import scattennet_amd as S
+    from scattennet_amd import ops, workloads as W
+    dev = torch.device("cuda:0")
+    torch.manual_seed(5)
+    B, T, d, H = 3, 96, 256, 16
+    cfg = W.model_cfg(d, H, 1, maxpos=T)
+    blocks = [S.CoordinateAttention(cfg, "self_attn"), S.CoordinateAttention(cfg, "self_attn")]
+    g = torch.Generator().manual_seed(7)
+    with torch.no_grad():
+        for blk in blocks:
+            for name, p in blk.named_parameters():
+                p.copy_(torch.randn(p.shape, generator=g) / (p.shape[-1] ** 0.5) if p.dim() == 2
+                        else (1.0 if name.endswith("weight") else 0.0) + 0.1 * torch.randn(p.shape, generator=g))
+    blocks = [b.to(dev) for b in blocks]
+    x = torch.randn(B, T, d, generator=g)
+    mask = torch.ones(B, T, dtype=torch.long)
+    mask[1, 60:] = 0
+    mask[2, 1:] = 0
+    g1, g2 = torch.randn(B, T, d, generator=g), torch.randn(B, T, d, generator=g)
+    xg = x.to(dev).requires_grad_(True)
+    kpm = S.key_padding_mask(mask.to(dev))
+    prof = ops.LaunchProfiler()
+    with prof:
+        h1 = blocks[0](xg, kpm)
+        h2 = blocks[1](h1, kpm)
+        loss = (h2 * g1.to(dev)).sum()
+        if second_consumer:
+            loss = loss + (h1 * g2.to(dev)).sum()
+        loss.backward()
+    torch.cuda.synchronize()
+    # hand-offs: block 1's FFN -> its attention LN; block 1's attention -> block 0's last LN;
+    # block 0's FFN -> its attention LN (block 0's attention input x has no fused producer)
+    assert prof.stats().get("gemm_lnb_kernel", {}).get("launches", 0) == 3
+
+    ps = [{k: v.detach().cpu().clone().requires_grad_(True) for k, v in blk.state_dict().items()} for blk in blocks]
+    xr = x.clone().requires_grad_(True)
+    am = O.additive_key_mask(mask)
+    r1 = O.coordinate_attention({"b." + k: v for k, v in ps[0].items()}, "b", xr, am, H, "self_attn")
+    r2 = O.coordinate_attention({"b." + k: v for k, v in ps[1].items()}, "b", r1, am, H, "self_attn")
+    ref = (r2 * g1).sum() + ((r1 * g2).sum() if second_consumer else 0.0)
+    assert rel_err(h2, r2) < PARITY_TOL
+    ref.backward()
+    assert rel_err(xg.grad, xr.grad) < PARITY_TOL
+    for blk, p in zip(blocks, ps):
+        gscale = max(float(v.grad.abs().max()) for v in p.values())
+        named = dict(blk.named_parameters())
+        for k, v in p.items():
+            assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))

@@ -67,49 +67,80 @@ def _encoder_oracle(enc, cfg, kp, mask, gout):
     return ref.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}
 
 
-def test_cfg3_full_encoder_vs_oracle():
-    """BASELINE config 3: yaml model section, 3 streams + residual + fusion, ragged masks.
+TIE_TOL = 1e-5  # |a - b| <= TIE_TOL * max(|a|, |b|, 0.1): below the fp32 forward error of either path
 
-    The residual network's ReLU + MaxPool1d make a few gradients discontinuous at fp32
-    resolution: at this seed right_encoder.residual.blocks.2 has max-pool pairs whose values
-    differ by 4e-6 at magnitude 6 (7e-7 relative), below the fp32 forward error of ANY
-    implementation, so which frame receives the gradient is a coin toss.  A gradient
-    therefore passes at PARITY_TOL, or — only where the oracle itself is that ill-conditioned —
-    within 2x the oracle's own spread when its inputs are perturbed at the fp32 level
-    (3e-5 relative, two samples)."""
+
+def _tie_aware_pool(o, gpu_in, stats):
+    """MaxPool1d(2, 2) over frames of the oracle's (B, T, C) block output, choosing the element
+    the GPU chose wherever the pair is an fp32-level tie (which element wins such a pair is
+    decided by forward rounding, not by the algorithm) and the oracle's own argmax elsewhere
+    (first element on exact equality, as torch's MaxPool1d)."""
+    a, b = o[:, 0::2], o[:, 1::2]
+    ga, gb = gpu_in[:, 0::2], gpu_in[:, 1::2]
+    mine, theirs = b > a, gb > ga
+    tie = (a - b).abs() <= TIE_TOL * torch.maximum(a.abs(), b.abs()).clamp(min=0.1)
+    stats["ties"] += int((tie & (a != b)).sum())
+    stats["flipped"] += int((tie & (mine != theirs)).sum())
+    stats["disagree_outside_ties"] += int((~tie & (mine != theirs)).sum())
+    return torch.where(torch.where(tie, theirs, mine), b, a)
+
+
+def test_cfg3_full_encoder_vs_oracle(monkeypatch):
+    """BASELINE config 3: yaml model section, 3 streams + residual + fusion, ragged masks;
+    output and EVERY gradient at the north-star 1e-3.
+
+    ReLU + MaxPool1d(2,2) make the gradient discontinuous at pairs whose two values are equal
+    to within fp32 forward rounding (at this seed e.g. right_encoder.residual.blocks.2 has
+    pairs 4e-6 apart at magnitude 6): which frame receives the gradient there is decided by
+    rounding in either implementation.  The oracle therefore pools such pairs (and only
+    those: |a - b| <= 1e-5 max(|a|, |b|, 0.1), detected and counted) the way the GPU did, from the
+    GPU's own pool inputs; outside them the two argmaxes must agree exactly.  No gradient
+    tolerance is relaxed."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
+    from scattennet_amd import ops
     torch.set_num_threads(min(16, torch.get_num_threads()))
     dev = torch.device("cuda:0")
     w = W.WORKLOADS["cfg3"]
     enc = W.build_encoder(w, dev, seed=4, init="random").eval()  # parity at eval (dropout off)
     kp, mask, gout = W.synthetic_batch(w, dev, seed=6, ragged=True)
+    pool_inputs = []  # per downsampling block: [body, left, right] (the grouped launch order)
+    fwd = ops.MaxPoolT.forward
+
+    def recording(ctx, G, *xs):
+        pool_inputs.append([x.detach().cpu() for x in xs])
+        return fwd(ctx, G, *xs)
+
+    monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(recording))
     fuse = enc(kp, mask)[0]
     fuse.backward(gout[0])
     torch.cuda.synchronize()
+    monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(fwd))
+    assert len(pool_inputs) == 2 and all(len(c) == 3 for c in pool_inputs)
+
     cfg = W.encoder_cfg(w)
-    kpc, mc, gc = kp.cpu(), mask.cpu(), gout[0].cpu()
-    ref, grads = _encoder_oracle(enc, cfg, kpc, mc, gc)
+    order = iter([(s, c) for s in range(3) for c in range(2)])  # oracle: body, left, right; blocks 0, 2
+    stats = {"ties": 0, "flipped": 0, "disagree_outside_ties": 0}
+    block = O.residual_block
+
+    def residual_block(p, prefix, x, in_dim, out_dim, downsample):
+        o = block(p, prefix, x, in_dim, out_dim, False)
+        if not downsample:
+            return o
+        s, c = next(order)
+        return _tie_aware_pool(o, pool_inputs[c][s], stats)
+
+    monkeypatch.setattr(O, "residual_block", residual_block)
+    ref, grads = _encoder_oracle(enc, cfg, kp.cpu(), mask.cpu(), gout[0].cpu())
+    print(f"cfg3 max-pool pairs: {stats}")
+    assert stats["disagree_outside_ties"] == 0, stats
     assert rel_err(fuse, ref) < PARITY_TOL
-    spread = {k: 0.0 for k in grads}
-    gen = torch.Generator().manual_seed(11)
-    for _ in range(2):
-        kp_p = kpc * (1 + 3e-5 * torch.randn(kpc.shape, generator=gen))
-        _, g_p = _encoder_oracle(enc, cfg, kp_p, mc, gc)
-        for k in grads:
-            spread[k] = max(spread[k], rel_err(g_p[k], grads[k]))
     gscale = max(float(t.abs().max()) for t in grads.values())
     named = dict(enc.named_parameters())
-    relaxed = []
     for k, gr in grads.items():
         assert named[k].grad is not None, k
         got = named[k].grad.cpu()
-        if close(got, gr, PARITY_TOL, gscale):
-            continue
-        e = rel_err(got, gr)
-        assert spread[k] > PARITY_TOL and e < 2 * spread[k], (k, e, spread[k])
-        relaxed.append(k)
-    assert len(relaxed) < len(grads) // 4, relaxed
+        assert close(got, gr, PARITY_TOL, gscale), (k, rel_err(got, gr))
     for k, prm in named.items():  # parameters the reference never trains (long shortcuts)
         if k not in grads:
             assert prm.grad is None, k
