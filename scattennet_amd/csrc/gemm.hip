@@ -545,6 +545,10 @@ struct LgCfg {
   static constexpr int A_BYTES = BM * GL_BK * 4;
   static constexpr int STAGE = A_BYTES + LG_B_BYTES;
   static constexpr int A_PIECES = BM / 8;  // 1-KiB DMA pieces of the A tile
+  // 32 rows: 8 waves (two per SIMD: one workgroup fills a CU's LDS), a 32x32 column block
+  // each; 16 rows: 4 waves, 64 columns each
+  static constexpr int NW = BM == 32 ? 8 : 4;
+  static constexpr int BPW = 32 / NW;      // B pieces (8 rows of 32 k) per wave per slice
 };
 
 struct GemmLnArgs {
@@ -567,7 +571,7 @@ __device__ __forceinline__ f32x4 lg_slot(const char* img, int r, int slot) {
 }
 
 template <int BM>
-__global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
+__global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmLnArgs args) {
   using CF = LgCfg<BM>;
   constexpr int S = CF::S;
   __shared__ __attribute__((aligned(1024))) char smem[S * CF::STAGE];
@@ -590,58 +594,56 @@ __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
   // apart do not — one source pointer per parity, stepped by 16 rows)
   const bool has_a = wave < CF::A_PIECES;
   const float* pa = lg_src(G.A, G.lda, m0, P.M, has_a ? wave : 0, lane);
-  const float* pb[2] = {lg_src(G.B, G.ldb, 0, P.N, 8 * wave, lane), lg_src(G.B, G.ldb, 0, P.N, 8 * wave + 1, lane)};
+  constexpr int BPW = CF::BPW;
+  const float* pb[2] = {lg_src(G.B, G.ldb, 0, P.N, BPW * wave, lane),
+                        lg_src(G.B, G.ldb, 0, P.N, BPW * wave + 1, lane)};
   const long pstep = 16L * G.ldb;
   auto dma = [&](int t, int stage) {
     char* base = smem + stage * CF::STAGE;
     const long kk = (long)t * GL_BK;
     if (has_a) gl_dma(pa + kk, base + wave * GL_PIECE);
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + CF::A_BYTES + (8 * wave + c) * GL_PIECE);
+    for (int c = 0; c < BPW; ++c)
+      gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + CF::A_BYTES + (BPW * wave + c) * GL_PIECE);
   };
 
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = G.alpha;
   if constexpr (BM == 32) {
-    f32x16 acc0, acc1;
+    f32x16 acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
     for (int i = 0; i < S - 1; ++i)
       if (i < total) dma(i, i);
     for (int t = 0; t < total; ++t) {
-      if (t + S - 2 < total) gl_wait_vm<9 * (S - 2)>();
-      else gl_wait_vm<0>();
+      if (t + S - 2 < total) {
+        if (has_a) gl_wait_vm<(BPW + 1) * (S - 2)>();
+        else gl_wait_vm<BPW * (S - 2)>();
+      } else {
+        gl_wait_vm<0>();
+      }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
       const char* As = smem + (t % S) * CF::STAGE;
       const char* Bs = As + CF::A_BYTES;
-      f32x4 fa[4], fb0[4], fb1[4];
+      f32x4 fa[4], fb[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         fa[g] = gl_frag<true>(As, 0, g, lane);
-        fb0[g] = gl_frag<true>(Bs, 64 * wave, g, lane);
-        fb1[g] = gl_frag<true>(Bs, 64 * wave + 32, g, lane);
+        fb[g] = gl_frag<true>(Bs, 32 * wave, g, lane);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc0 = mfma32(fa[g][j], fb0[g][j], acc0);
-          acc1 = mfma32(fa[g][j], fb1[g][j], acc1);
-        }
+        for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
     }
     // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
     __syncthreads();
     const int col = lane & 31, rowh = 4 * (lane >> 5);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = (r & 3) + 8 * (r >> 2) + rowh;
-      V[m * LG_VS + 64 * wave + col] = acc0[r] * alpha;
-      V[m * LG_VS + 64 * wave + 32 + col] = acc1[r] * alpha;
-    }
+    for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
   } else {
     // 16 rows: wave w owns columns 64w .. 64w+63 as four 16x16 accumulators; per 16-k group
     // c a lane reads 4 consecutive k of its A row and of each B row (one float4 each)
@@ -677,9 +679,9 @@ __global__ __launch_bounds__(256) void gemm_ln_kernel(const GemmLnArgs args) {
   }
   __syncthreads();
 
-  // each wave normalises BM/4 rows at once: every row is 64 lanes x float4 (coalesced), and
+  // each wave normalises BM/NW rows at once: every row is 64 lanes x float4 (coalesced), and
   // the rows' reductions are interleaved (independent shuffle chains, one latency each)
-  constexpr int RPW = BM / 4;
+  constexpr int RPW = BM / CF::NW;
   const int n = 4 * lane;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
@@ -1364,18 +1366,17 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
     maxM = maxM > P.M ? maxM : P.M;
   }
   if (maxM == 0) return SCA_OK;
-  // 16-row tiles (2 workgroups / CU) unless the reduction is long and 32-row tiles already
-  // give a workgroup per CU (measured: tools/gemm_ln_bench.py, bench.py A/B)
+  // 32-row tiles (8 waves) whenever they give a workgroup per CU, else 16-row tiles (2
+  // workgroups / CU): tools/gemm_ln_bench.py 4x(2048,256,K): K = 768 41.0 vs 44.6 us,
+  // K = 256 19.8 vs 20.8 us; 1x(2048,256,256): 15.2 vs 10.9 us
   static const int bm_env = getenv("SCA_GEMM_LN_BM") ? atoi(getenv("SCA_GEMM_LN_BM")) : 0;
-  int maxK = 0;
-  for (int i = 0; i < nprob; ++i) maxK = maxK > probs[i].seg[0].K ? maxK : probs[i].seg[0].K;
   const long wg32 = (long)nprob * ((maxM + 31) / 32);
-  const int bm = bm_env ? bm_env : ((maxK > 512 && wg32 >= 256) ? 32 : 16);
+  const int bm = bm_env ? bm_env : (wg32 >= 256 ? 32 : 16);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (bm == 16) {
     hipLaunchKernelGGL(gemm_ln_kernel<GL_A16>, dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(gemm_ln_kernel<GL_A32>, dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gemm_ln_kernel<GL_A32>, dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;

@@ -209,8 +209,7 @@ def gemm_ln(probs, lns, eps):
         flops = sum(2.0 * p.M * p.N * p.seg[0].K for p in chunk) if _PROFILER else 0.0
         # the row-tile variant sca_gemm_ln picks (gemm.hip), for the kernel name rocprofv3 shows
         bm = int(__import__("os").environ.get("SCA_GEMM_LN_BM", "0")) or (
-            32 if (max(p.seg[0].K for p in chunk) > 512 and
-                   len(chunk) * ((max(p.M for p in chunk) + 31) // 32) >= 256) else 16)
+            32 if len(chunk) * ((max(p.M for p in chunk) + 31) // 32) >= 256 else 16)
         with _timed(f"gemm_ln_kernel<{bm}>", flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
