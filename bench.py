@@ -230,33 +230,87 @@ def describe(w):
             f"B={w['B']} T={w['T']} K={w['K_all']} d={w['d']} H={w['H']}, fwd+bwd all params")
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _time_oracle(w, plist, groups, cfg, B, iters, warm=1):
+    """Median seconds of `iters` oracle fwd+bwd steps over the first B clips (after `warm`)."""
+    from oracle import sca_oracle as O
+    kp, mask, gout = W.synthetic_batch(dict(w, B=B), "cpu", seed=1)
+    times = []
+    for i in range(warm + iters):
+        t0 = time.perf_counter()
+        outs = O.multi_stream_sca(plist, kp, mask, groups, cfg)
+        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+        dt = time.perf_counter() - t0
+        for p in plist:
+            for v in p.values():
+                v.grad = None
+        if i >= warm:
+            times.append(dt)
+    times.sort()
+    return times[len(times) // 2]
+
+
+def _time_cfg1(iters, warm=2):
+    """Median seconds of the config-1 x-stream fwd+bwd (oracle.x_stream) on this host."""
+    from oracle import sca_oracle as O
+    w1 = W.WORKLOADS["cfg1"]
+    mod = W.build_streams(w1, "cpu", seed=0, init="reference").streams[0]
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in mod.state_dict().items()}
+    cfg = W.model_cfg(w1["d"], w1["H"], w1["L"], maxpos=w1["maxpos"])
+    kp, mask, _ = W.synthetic_batch(w1, "cpu", seed=1)
+    g = torch.randn(w1["B"], w1["T"], w1["d"], generator=torch.Generator().manual_seed(1))
+    times = []
+    for i in range(warm + iters):
+        t0 = time.perf_counter()
+        (O.x_stream(p, "", kp, mask, cfg) * g).sum().backward()
+        times.append(time.perf_counter() - t0)
+        for v in p.values():
+            v.grad = None
+    times = sorted(times[warm:])
+    return times[len(times) // 2]
+
+
 def cpu_baseline(w, model, budget_s):
     """The CPU oracle (oracle/sca_oracle.py, pinned to the reference's golden vectors) timed
-    on this host: same workload, same weights, a bounded number of fwd+bwd iterations."""
-    from oracle import sca_oracle as O
+    on this host (BASELINE.md CPU-baseline plan): same workload and weights, 1 warm-up then
+    the median of >= 3 fwd+bwd steps on all the box's threads; a 1-thread run on a 1-clip
+    sample; config 1 (x-stream, B=2 T=64 K=27 d=64) at both thread counts.  About 15-20 s
+    of CPU time in all (`budget_s` is kept for the command line; the sample sizes are fixed)."""
     threads = os.cpu_count() or 1
-    # the GPU box reports the whole machine; use the box's CPU share (16) at most
-    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
-    torch.set_num_threads(threads)
+    # the GPU box reports the whole machine; use the box's CPU share (OMP_NUM_THREADS = 16)
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", "16")))
     cfg = W.model_cfg(w["d"], w["H"], w["L"], maxpos=w["maxpos"])
     groups = W.split_groups(w["groups"])
     plist = [{k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
              for m in model.streams]
-    kp, mask, gout = W.synthetic_batch(w, "cpu", seed=1)
-    iters = 0
-    t0 = time.perf_counter()
-    while True:
-        outs = O.multi_stream_sca(plist, kp, mask, groups, cfg)
-        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
-        for p in plist:
-            for v in p.values():
-                v.grad = None
-        iters += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(w["B"] * iters / dt, 3), "unit": "clips/s", "cores": threads, "kind": "port",
-            "sample": f"{iters} fwd+bwd step(s) of the full workload (B={w['B']}) on the CPU oracle, {dt:.1f} s"}
+    torch.set_num_threads(threads)
+    t_full = _time_oracle(w, plist, groups, cfg, w["B"], iters=3)
+    torch.set_num_threads(1)
+    t_one = _time_oracle(w, plist, groups, cfg, 1, iters=3)
+    c1_one = _time_cfg1(iters=9)
+    torch.set_num_threads(threads)
+    c1_full = _time_cfg1(iters=9)
+    w1 = W.WORKLOADS["cfg1"]
+    return {"value": round(w["B"] / t_full, 3), "unit": "clips/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
+            "sample": f"median of 3 fwd+bwd steps of the full workload (B={w['B']}) on the CPU oracle after 1 warm-up, "
+                      f"{threads} threads ({t_full:.2f} s/step)",
+            "one_thread": {"value": round(1 / t_one, 3), "unit": "clips/s", "cores": 1,
+                           "sample": f"median of 3 fwd+bwd steps of 1 clip of the same workload ({t_one:.2f} s/step)"},
+            "cfg1": {"value": round(w1["B"] / c1_full, 2), "one_thread": round(w1["B"] / c1_one, 2), "unit": "clips/s",
+                     "sample": "BASELINE config 1: x-stream (mapping + 4 self layers), B=2 T=64 K=27 d=64 H=4, median "
+                               f"of 9 fwd+bwd steps ({1e3 * c1_full:.1f} ms at {threads} threads, "
+                               f"{1e3 * c1_one:.1f} ms at 1)"}}
 
 
 if __name__ == "__main__":

@@ -389,12 +389,34 @@ __device__ __forceinline__ f32x4 gl_frag(const char* img, int r0, int g, int lan
   return v;
 }
 
+#ifdef SCA_GEMM_STAMPS
+// Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at
+// entry, first slice landed, main loop done, epilogue done -> tools/gemm_stamps.py
+constexpr int STAMP_MAX = 16384;
+__device__ unsigned long long g_stamps[STAMP_MAX][5];
+#define SCA_STAMP(slot)                                                            \
+  do {                                                                             \
+    if (threadIdx.x == 0 && stamp_id < STAMP_MAX) {                                \
+      g_stamps[stamp_id][slot] = __builtin_amdgcn_s_memrealtime();                 \
+    }                                                                              \
+  } while (0)
+#else
+#define SCA_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 template <int LAYOUT, int S>
 __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
   constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
   constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
   constexpr int STAGE = 2 * GL_OP_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+#ifdef SCA_GEMM_STAMPS
+  const unsigned stamp_id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (threadIdx.x == 0 && stamp_id < STAMP_MAX) g_stamps[stamp_id][4] = (unsigned long long)__smid();
+#endif
+  SCA_STAMP(0);
 
   const unsigned gx = gridDim.x, gy = gridDim.y;
   const unsigned nwg = gx * gy * gridDim.z;
@@ -476,6 +498,9 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
     else gl_wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // every wave's pieces of slice t landed; slice t-1 fully read
     __builtin_amdgcn_sched_barrier(0);
+#ifdef SCA_GEMM_STAMPS
+    if (t == 0) SCA_STAMP(1);
+#endif
     if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
     const char* As = smem + (t % S) * STAGE;
     const char* Bs = As + GL_OP_BYTES;
@@ -504,6 +529,170 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
       args.ws[args.bias_off[pid] + (long)ks * P.M + m0 + threadIdx.x] = bsum * alpha;
     else
       P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
+  }
+  if (alpha != 1.f) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] *= alpha;
+  }
+  if (splitk > 1) {
+    float* slab = args.ws + args.slab_off[pid] + (long)ks * P.M * P.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + rowh;
+      const int n = n0 + wn + col;
+      if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[r];
+    }
+    return;
+  }
+  SCA_STAMP(2);
+  const f32x16 accs[1][1] = {{acc}};
+  epilogue_block<1, 1>(P, accs, m0 + wm, n0 + wn, col, rowh, args.drop_off);
+#ifdef SCA_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  SCA_STAMP(3);
+}
+
+// ------------------------------------------------------------------------------ LDS-DMA, 8 waves
+// gemm_glds_kernel's 64x64 tile with TWO 4-wave groups that split the K-slices of the tile
+// between them (group g computes slices g, g+2, ...; the ring stage holds one slice per
+// group, each exactly gemm_glds_kernel's slice image, DMA'd by its own group); the groups'
+// accumulators are summed through LDS before the epilogue.  For long-K launches with few
+// tiles (the weight gradients: 16 x (256 x 256) at K = B*T = 2048 are 256 tiles, one per CU)
+// it gives two waves per SIMD without split-K slabs or a reduce launch.
+template <int LAYOUT, int S>
+__global__ __launch_bounds__(512) void gemm_glds2_kernel(const GemmArgs args) {
+  constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
+  constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
+  constexpr int SLICE = 2 * GL_OP_BYTES;  // one group's slice image (A then B)
+  constexpr int STAGE = 2 * SLICE;
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
+
+  const int splitk = args.splitk;
+  const int pid = bz / splitk;
+  const int ks = bz % splitk;
+  const sca_gemm_problem& P = args.p[pid];
+  const int m0 = by * GL_BM, n0 = bx * GL_BN;
+  if (m0 >= P.M || n0 >= P.N) return;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = wave >> 2, w4 = wave & 3;  // K-slice group, wave within the group
+  const int wm = (w4 >> 1) * 32, wn = (w4 & 1) * 32;
+
+  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
+    seg_kbeg[s] = seg_n[s] = 0;
+    if (s < P.nseg) {
+      int kbeg = 0, kend = P.seg[s].K;
+      if (splitk > 1) {
+        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + GL_BK - 1) / GL_BK * GL_BK;
+        kbeg = ks * chunk;
+        kend = min(P.seg[s].K, kbeg + chunk);
+      }
+      seg_kbeg[s] = kbeg;
+      seg_n[s] = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
+      total += seg_n[s];
+    }
+  }
+  const int pairs = (total + 1) / 2;  // ring stages to walk; group g owns slice 2p + g
+  int iseg = -1, tseg0 = 0, tend = 0;
+  const float* pa[2] = {nullptr, nullptr};
+  const float* pb[2] = {nullptr, nullptr};
+  long stepA = 0, stepB = 0;
+  auto dma = [&](int p, int stage) {  // this group's slice of stage p (slices issued in order)
+    const int t = 2 * p + grp;
+    if (t >= total) return;
+    while (t >= tend) {
+      ++iseg;
+      tseg0 = tend;
+      tend += seg_n[iseg];
+      const sca_gemm_seg& G = P.seg[iseg];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        pa[c] = gl_src<A_KC>(G.A, G.lda, m0, P.M, seg_kbeg[iseg], c, w4, lane);
+        pb[c] = gl_src<B_KC>(G.B, G.ldb, n0, P.N, seg_kbeg[iseg], c, w4, lane);
+      }
+      stepA = A_KC ? GL_BK : (long)GL_BK * G.lda;
+      stepB = B_KC ? GL_BK : (long)GL_BK * G.ldb;
+    }
+    const long kk = t - tseg0;
+    char* base = smem + stage * STAGE + grp * SLICE;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      gl_dma(pa[c] + kk * stepA, base + gl_dst<A_KC>(c, w4));
+      gl_dma(pb[c] + kk * stepB, base + GL_OP_BYTES + gl_dst<B_KC>(c, w4));
+    }
+  };
+
+  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && bx == 0;
+  float bsum = 0.f;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < pairs) dma(i, i);
+  for (int p = 0; p < pairs; ++p) {
+    // each wave issued 4 DMAs per stage in which its group has a slice; S-2 younger stages
+    // may stay in flight except at the tail, where a group may have issued fewer
+    if (p + S - 2 < pairs && 2 * (p + S - 2) + 1 < total) gl_wait_vm<4 * (S - 2)>();
+    else gl_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (p + S - 1 < pairs) dma(p + S - 1, (p + S - 1) % S);
+    if (2 * p + grp < total) {
+      const char* As = smem + (p % S) * STAGE + grp * SLICE;
+      const char* Bs = As + GL_OP_BYTES;
+      if (do_bias && w4 == 0) {
+        const float* af = (const float*)As;  // TN: A image is [32 k][64 m]
+#pragma unroll 8
+        for (int k = 0; k < GL_BK; ++k) bsum += af[k * 64 + lane];
+      }
+      f32x4 fa[4], fb[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        fa[g] = gl_frag<A_KC>(As, wm, g, lane);
+        fb[g] = gl_frag<B_KC>(Bs, wn, g, lane);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
+    }
+  }
+  // group 1 hands its partial tile (and bias partial) to group 0 through the freed ring
+  __syncthreads();
+  float* X = reinterpret_cast<float*>(smem);
+  if (grp == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) X[(w4 * 16 + r) * 64 + lane] = acc[r];
+    if (w4 == 0) X[4 * 16 * 64 + lane] = bsum;
+  }
+  __syncthreads();
+  if (grp == 1) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += X[(w4 * 16 + r) * 64 + lane];
+  if (w4 == 0) bsum += X[4 * 16 * 64 + lane];
+
+  const float alpha = P.seg[0].alpha;
+  const int col = lane & 31;
+  const int rowh = 4 * (lane >> 5);
+  if (do_bias && w4 == 0 && m0 + lane < P.M) {
+    if (splitk > 1)
+      args.ws[args.bias_off[pid] + (long)ks * P.M + m0 + lane] = bsum * alpha;
+    else
+      P.bias_grad[m0 + lane] = bsum * alpha * P.bias_grad_scale;
   }
   if (alpha != 1.f) {
 #pragma unroll
@@ -1182,6 +1371,13 @@ int launch_glds(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
+template <int LAYOUT, int S>
+int launch_glds2(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
+  hipLaunchKernelGGL((gemm_glds2_kernel<LAYOUT, S>), grid, dim3(512), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (tile > 10 && tile < 20 && !persistent_ok(a, nprob)) tile = 1;
@@ -1190,6 +1386,8 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
     case 20: return launch_glds<LAYOUT, 3>(a, nprob, maxM, maxN, st);
     case 21: return launch_glds<LAYOUT, 2>(a, nprob, maxM, maxN, st);
     case 22: return launch_glds<LAYOUT, 4>(a, nprob, maxM, maxN, st);
+    case 23: return launch_glds2<LAYOUT, 3>(a, nprob, maxM, maxN, st);
+    case 24: return launch_glds2<LAYOUT, 2>(a, nprob, maxM, maxN, st);
     case 11: return launch_persistent<LAYOUT, T1>(a, nprob, st);
     case 12: return launch_persistent<LAYOUT, T2>(a, nprob, st);
     case 13: return launch_persistent<LAYOUT, T3>(a, nprob, st);
@@ -1225,8 +1423,15 @@ int pick_tile(int layout, long tiles64, int splitk) {
 
 }  // namespace
 
+#ifdef SCA_GEMM_STAMPS
+extern "C" int sca_gemm_stamps(unsigned long long* out, int n) {
+  if (n > STAMP_MAX) n = STAMP_MAX;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 5 * n) == hipSuccess ? 0 : 3;
+}
+#endif
+
 extern "C" int sca_gemm_tile_override(int layout, int tile) {
-  if (layout < 0 || layout > 2 || tile < 0 || (tile > kNumTiles && (tile < 11 || tile > 16) && (tile < 20 || tile > 22)))
+  if (layout < 0 || layout > 2 || tile < 0 || (tile > kNumTiles && (tile < 11 || tile > 16) && (tile < 20 || tile > 24)))
     return SCA_ERR_ARG;
   g_tile_override[layout] = tile;
   return SCA_OK;

@@ -103,3 +103,8 @@ def test_position_table_overflow_raises():
     p = {"t": torch.zeros(6, 4)}
     with pytest.raises(IndexError):
         O.position_embed(p, "t", torch.zeros(1, 5, 4))
+
+
+def test_xstream_cfg1():
+    """BASELINE config 1's x-coordinate stream (the CPU baseline's config-1 workload)."""
+    _run("xstream_cfg1", lambda p, i, m: O.x_stream(p, "", i["keypoints"], i["mask"], m["cfg"]), ("keypoints",))

@@ -13,7 +13,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 9: "64bk16", 20: "G64s3", 21: "G64s2", 22: "G64s4", 11: "P64x64", 12: "P128x64", 14: "P128sq", 15: "P128sq8w", 16: "P128x64w8"}
+TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 9: "64bk16", 20: "G64s3", 21: "G64s2", 22: "G64s4", 23: "G2x64s3",
+         24: "G2x64s2", 11: "P64x64", 12: "P128x64", 14: "P128sq", 15: "P128sq8w", 16: "P128x64w8"}
 
 
 def make_case(name, layout, shapes, splitk=1, segs=1):
@@ -75,6 +76,10 @@ def main():
         make_case("TN dW 12x(256,256,2048) sk2", L.GEMM_TN, [(d, d, M)] * 12, splitk=2),
         make_case("NT as-dW 12x(256,256,2048) sk4", L.GEMM_NT, [(d, d, M)] * 12, splitk=4),
         make_case("TN dW 12x(256,256,2048) sk1", L.GEMM_TN, [(d, d, M)] * 12, splitk=1),
+        make_case("TN dW 16x(256,256,2048) sk1", L.GEMM_TN, [(d, d, M)] * 16, splitk=1),
+        make_case("TN dW 16x(256,256,2048) sk3", L.GEMM_TN, [(d, d, M)] * 16, splitk=3),
+        make_case("TN dW 16x(256,256,2048) sk2", L.GEMM_TN, [(d, d, M)] * 16, splitk=2),
+        make_case("TN dW12 8x(mixed,2048) sk1", L.GEMM_TN, [(d, F, M)] * 4 + [(F, d, M)] * 4, splitk=1),
         make_case("TN dW2 4x(256,768,2048) sk4", L.GEMM_TN, [(d, F, M)] * 4, splitk=4),
         make_case("TN dW2 4x(256,768,2048) sk2", L.GEMM_TN, [(d, F, M)] * 4, splitk=2),
         # steady-state main loop (long K): 512 and 1536 64x64 tiles
