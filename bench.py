@@ -121,6 +121,8 @@ def main():
     if not args.no_graph:
         for p in params:
             p.grad = None
+        if reducer is not None:
+            reducer.quiesce()  # no eager RCCL work left for the watchdog to poll during capture
         graph = torch.cuda.CUDAGraph()
         # thread-local capture mode with RCCL: ProcessGroupNCCL's watchdog thread queries the
         # warm-up steps' events while the step is captured (tools/dp_capture_diag.py)

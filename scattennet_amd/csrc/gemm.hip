@@ -180,6 +180,71 @@ __device__ __forceinline__ void epilogue_block(const sca_gemm_problem& P, const 
     }
 }
 
+// Row-form epilogue of one wave's 32x32 accumulator (the LDS-DMA kernels): the tile is
+// transposed through a wave-private LDS scratch (row stride 40 floats: the two half-waves'
+// rows 4 apart land 128 B apart, conflict-free) so that each lane owns 4 float4 row pieces
+// (rows lane/8 + 8i, columns 4*(lane%8)) and every epilogue load / store is 16 B per lane —
+// a quarter of the store instructions of the per-element form (the epilogue tail of these
+// short-K launches is store-issue-bound).  Requires N % 4 == 0 (glds_ok).
+constexpr int EPI_LD = 40;
+
+__device__ __forceinline__ void acc_to_rows(const f32x16& acc, float* scratch, int lane, f32x4 (&v)[4]) {
+  const int col = lane & 31, rowh = 4 * (lane >> 5);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) scratch[((r & 3) + 8 * (r >> 2) + rowh) * EPI_LD + col] = acc[r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = ld4(scratch + ((lane >> 3) + 8 * i) * EPI_LD + 4 * (lane & 7));
+}
+
+// v = (acc + bias) * post_scale; GELU (keeps the pre-activation) / dropout / GELU'; + resid
+// (+ C_old): exactly epilogue()'s order, on float4 row pieces
+__device__ __forceinline__ void epilogue_rows(const sca_gemm_problem& P, const f32x4 (&v)[4], int mb, int nb, int lane,
+                                              const unsigned long long* drop_off) {
+  const int n = nb + 4 * (lane & 7);
+  if (n >= P.N) return;
+  DropMask dm;
+  if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, drop_off);
+  const f32x4 bias = P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mb + (lane >> 3) + 8 * i;
+    if (m >= P.M) continue;
+    f32x4 ex = {0.f, 0.f, 0.f, 0.f}, ax = ex;
+    if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
+    if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
+    if (P.epi & SCA_EPI_DGELU) ax = ld4(P.aux + (long)m * P.ldx + n);
+    f32x4 o = (v[i] + bias) * P.post_scale;
+    if (P.epi & SCA_EPI_GELU) {
+      st4(P.aux_out + (long)m * P.ldo + n, o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
+    }
+    if (P.epi & SCA_EPI_DROPOUT) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), o[j]);
+    }
+    if (P.epi & SCA_EPI_DGELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
+    }
+    st4(P.C + (long)m * P.ldc + n, o + ex);
+  }
+}
+
+// split-K partial slab of the same tile, float4 rows
+__device__ __forceinline__ void slab_rows(float* slab, const f32x4 (&v)[4], int M, int N, int mb, int nb, int lane) {
+  const int n = nb + 4 * (lane & 7);
+  if (n >= N) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mb + (lane >> 3) + 8 * i;
+    if (m < M) st4(slab + (long)m * N + n, v[i]);
+  }
+}
+
 template <int LAYOUT, class C>
 __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NT = C::NT, RM = C::RM, RN = C::RN;
@@ -534,19 +599,19 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] *= alpha;
   }
+  SCA_STAMP(2);
+  (void)col;
+  (void)rowh;
+  // the ring is free once every wave has passed its last slice: wave-private transposition
+  // scratch for the row-form epilogue (4 x 5 KB)
+  __syncthreads();
+  f32x4 rows[4];
+  acc_to_rows(acc, reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD, lane, rows);
   if (splitk > 1) {
-    float* slab = args.ws + args.slab_off[pid] + (long)ks * P.M * P.N;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + rowh;
-      const int n = n0 + wn + col;
-      if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[r];
-    }
+    slab_rows(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N, rows, P.M, P.N, m0 + wm, n0 + wn, lane);
     return;
   }
-  SCA_STAMP(2);
-  const f32x16 accs[1][1] = {{acc}};
-  epilogue_block<1, 1>(P, accs, m0 + wm, n0 + wn, col, rowh, args.drop_off);
+  epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 #ifdef SCA_GEMM_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -698,18 +763,15 @@ __global__ __launch_bounds__(512) void gemm_glds2_kernel(const GemmArgs args) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] *= alpha;
   }
+  (void)col;
+  (void)rowh;
+  f32x4 rows[4];  // transposition scratch past the hand-off buffer X
+  acc_to_rows(acc, reinterpret_cast<float*>(smem + 20 * 1024) + w4 * 32 * EPI_LD, lane, rows);
   if (splitk > 1) {
-    float* slab = args.ws + args.slab_off[pid] + (long)ks * P.M * P.N;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + rowh;
-      const int n = n0 + wn + col;
-      if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[r];
-    }
+    slab_rows(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N, rows, P.M, P.N, m0 + wm, n0 + wn, lane);
     return;
   }
-  const f32x16 accs[1][1] = {{acc}};
-  epilogue_block<1, 1>(P, accs, m0 + wm, n0 + wn, col, rowh, args.drop_off);
+  epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 }
 
 // ------------------------------------------------------------------------------ GEMM + LayerNorm

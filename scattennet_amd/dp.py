@@ -243,6 +243,18 @@ class GradBuckets:
         if self.average:
             self.flat.mul_(1.0 / self.world)
 
+    def quiesce(self, seconds=0.5):
+        """Call before capturing a step into a hipGraph: completes every eager collective and
+        gives ProcessGroupNCCL's watchdog thread (it polls every 100 ms) time to retire them
+        — a watchdog query of a pending eager work's event while the graph is being captured
+        aborts the process (tools/dp_capture_diag.py, variant "reducer")."""
+        import time
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize()
+        time.sleep(seconds)
+
     def bucket_sizes(self):
         return [n * 4 for _, n, _ in (self.plan or [])]
 

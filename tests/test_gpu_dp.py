@@ -109,6 +109,7 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
         eager = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
         for p in params:
             p.grad = None
+        red.quiesce()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # RCCL watchdog thread
             outs = model(kp, mask)
