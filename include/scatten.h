@@ -115,6 +115,16 @@ int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* probs, int s
                      void* stream);
 int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                     void* stream);
+/* Split-K with the slab combine inside the GEMM launch (no second launch): every split writes
+ * its partial slab write-through and takes a ticket on its output tile's counter; the last
+ * arriver sums the slabs in slice order (deterministic) and runs the epilogue.
+ * `counters`: sca_gemm_splitk_counters(nprob, max M, max N) unsigned ints, ZERO on entry and
+ * left zero on exit (the last arriver resets its tile's counter), so one zeroed buffer serves
+ * any number of launches that do not run concurrently on the same counters.  Falls back to
+ * the two-launch form when the LDS-DMA kernel cannot take the shapes.                      */
+long sca_gemm_splitk_counters(int nprob, int maxM, int maxN);
+int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                          unsigned* counters, void* stream);
 
 /* NT GEMM + post-LN LayerNorm in one launch (d_model = 256): per problem
  *   C = resid + dropout((A B^T + bias) * post_scale)      (exactly sca_gemm's NT epilogue)

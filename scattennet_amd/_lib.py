@@ -109,6 +109,8 @@ EXPORTS = {
     "sca_gemm_partial": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "sca_gemm_reduce": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "sca_gemm_tile_override": ([c_int, c_int], c_int),
+    "sca_gemm_splitk_counters": ([c_int, c_int, c_int], c_long),
+    "sca_gemm_splitk_fused": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_lnb_blocks": ([c_int], c_int),
@@ -147,6 +149,7 @@ EXPORTS = {
 }
 
 _lib = None
+MISSING = set()  # entry points an alternative build (SCA_LIB_PATH) does not export
 
 
 def lib():
@@ -157,7 +160,11 @@ def lib():
             raise RuntimeError(f"scattennet_amd: {LIB_PATH} is missing — run __graft_entry__.build() "
                                "(make -C scattennet_amd/csrc).  There is no fallback path.")
         L = ctypes.CDLL(LIB_PATH)
+        alternative = os.environ.get("SCA_LIB_PATH") is not None
         for name, (argt, rest) in EXPORTS.items():
+            if alternative and not hasattr(L, name):  # an older A/B build: entry points it lacks
+                MISSING.add(name)
+                continue
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest

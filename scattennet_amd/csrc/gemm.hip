@@ -37,6 +37,7 @@ struct GemmArgs {
   const unsigned long long* drop_off;           // dropout step counter (sca_dropout_offset)
   long slab_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first partial slab in ws
   long bias_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first bias partial row in ws
+  unsigned* counters;                           // split-K combined in-launch (sca_gemm_splitk_fused)
 };
 
 // Workgroup tile configuration.
@@ -454,6 +455,37 @@ __device__ __forceinline__ f32x4 gl_frag(const char* img, int r0, int g, int lan
   return v;
 }
 
+// ---- in-launch split-K combine (write-through slabs + arrival ticket, last arriver sums) ----
+// MI355X_MICROARCH.md § inter-workgroup visibility / cdna_hip_programming.md §6 G16 R1: the slab
+// bytes are stored write-through (sc1, buffer stores with aux = 16), every storing wave drains
+// (vmcnt 0) before the workgroup's barrier, ONE lane takes a ticket (relaxed agent-scope
+// atomic add on the tile's counter); the workgroup that draws splitk - 1 reads every slab with
+// sc1 loads (no acquire fence needed for sc1-stored, sc1-loaded bytes), in slice order 0 ..
+// splitk-1 whichever arrived last (deterministic), resets the counter to 0 and runs the
+// epilogue.  Correct for any placement of a tile's slices over XCDs / CUs.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void slab_rows_sc1(float* slab_base, long slab_floats, const f32x4 (&v)[4], int M, int N,
+                                              int mb, int nb, int lane, long off0) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab_base, 0, (int)(slab_floats * 4), 0x00020000);
+  const int n = nb + 4 * (lane & 7);
+  if (n >= N) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mb + (lane >> 3) + 8 * i;
+    if (m < M) {
+      const f32x4 x = v[i];
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs,
+                                             (int)((off0 + (long)m * N + n) * 4), 0, 16);
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, long float_off) {
+  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(float_off * 4), 0, 16);
+  return *reinterpret_cast<const f32x4*>(&r);
+}
+
 #ifdef SCA_GEMM_STAMPS
 // Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at
 // entry, first slice landed, main loop done, epilogue done -> tools/gemm_stamps.py
@@ -587,11 +619,13 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
   }
 
   const float alpha = P.seg[0].alpha;
-  const int col = lane & 31;
-  const int rowh = 4 * (lane >> 5);
+  const bool fused_k = splitk > 1 && args.counters != nullptr;  // in-launch split-K combine
   if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
-    if (splitk > 1)
-      args.ws[args.bias_off[pid] + (long)ks * P.M + m0 + threadIdx.x] = bsum * alpha;
+    float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m0 + threadIdx.x;
+    if (fused_k)
+      __hip_atomic_store(bp, bsum * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
+    else if (splitk > 1)
+      *bp = bsum * alpha;
     else
       P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
   }
@@ -600,13 +634,45 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
     for (int r = 0; r < 16; ++r) acc[r] *= alpha;
   }
   SCA_STAMP(2);
-  (void)col;
-  (void)rowh;
   // the ring is free once every wave has passed its last slice: wave-private transposition
   // scratch for the row-form epilogue (4 x 5 KB)
   __syncthreads();
   f32x4 rows[4];
   acc_to_rows(acc, reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD, lane, rows);
+  if (fused_k) {
+    const long MN = (long)P.M * P.N;
+    float* slabs = args.ws + args.slab_off[pid];
+    slab_rows_sc1(slabs, (long)splitk * MN, rows, P.M, P.N, m0 + wm, n0 + wn, lane, (long)ks * MN);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(smem + 20 * 1024);  // one LDS array (trap 4a)
+    unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded: no agent acquire
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
+    const int n = n0 + wn + 4 * (lane & 7);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = min(m0 + wm + (lane >> 3) + 8 * i, P.M - 1);
+      const long e = (long)m * P.N + min(n, P.N - 4);
+      f32x4 t = ld4_sc1(rs, e);
+      for (int s2 = 1; s2 < splitk; ++s2) t += ld4_sc1(rs, s2 * MN + e);
+      rows[i] = t;
+    }
+    if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
+      float* bp = args.ws + args.bias_off[pid] + m0 + threadIdx.x;
+      float t = 0.f;
+      for (int s2 = 0; s2 < splitk; ++s2)
+        t += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P.bias_grad[m0 + threadIdx.x] = t * P.bias_grad_scale;
+    }
+    epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
+    return;
+  }
   if (splitk > 1) {
     slab_rows(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N, rows, P.M, P.N, m0 + wm, n0 + wn, lane);
     return;
@@ -1352,6 +1418,33 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args,
   P.C[(long)m * P.ldc + n] = epilogue(P, m, n, v, args.drop_off);
 }
 
+// The same, four consecutive elements per thread (N % 4 == 0): 16-B slab loads and C stores.
+// blockIdx.x < nc4: C elements 4e .. 4e+3; beyond: the bias partials (one per thread).
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GemmArgs args, int nc4) {
+  const sca_gemm_problem& P = args.p[blockIdx.y];
+  const long MN = (long)P.M * P.N;
+  if ((int)blockIdx.x >= nc4) {
+    const long m = (long)(blockIdx.x - nc4) * 256 + threadIdx.x;
+    if (P.bias_grad && m < P.M) {
+      const float* bp = args.ws + args.bias_off[blockIdx.y] + m;
+      float v = 0.f;
+      for (int s = 0; s < args.splitk; ++s) v += bp[(long)s * P.M];
+      P.bias_grad[m] = v * P.bias_grad_scale;
+    }
+    return;
+  }
+  const long e = 4 * ((long)blockIdx.x * 256 + threadIdx.x);
+  if (e >= MN) return;
+  const int m = (int)(e / P.N), n = (int)(e % P.N);
+  const float* slab = args.ws + args.slab_off[blockIdx.y] + e;
+  f32x4 v = ld4(slab);
+  for (int s = 1; s < args.splitk; ++s) v += ld4(slab + s * MN);
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = epilogue(P, m, n + j, v[j], args.drop_off);
+  st4(P.C + (long)m * P.ldc + n, o);
+}
+
 int pick_grid(int tiles, int max_per_cu) {
   int best_w = 1;
   long best = -1;
@@ -1504,7 +1597,7 @@ extern "C" void sca_set_error(const char* msg);
 namespace {
 // do_main: the GEMM launch; do_reduce: the split-K slab reduction (splitk > 1 only)
 int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace, void* stream,
-              bool do_main, bool do_reduce) {
+              bool do_main, bool do_reduce, unsigned* counters = nullptr) {
   if (nprob <= 0) return SCA_OK;
   if (nprob > SCA_GEMM_MAX_PROBLEMS || layout < 0 || layout > 2 || splitk < 1) {
     sca_set_error("sca_gemm: bad nprob/layout/splitk");
@@ -1514,6 +1607,7 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   a.splitk = splitk;
   a.ws = workspace;
   a.drop_off = sca_drop_offset_ptr();
+  a.counters = nullptr;
   int maxM = 0, maxN = 0;
   for (int i = 0; i < nprob; ++i) {
     const sca_gemm_problem& P = probs[i];
@@ -1569,6 +1663,11 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   long tiles64 = 0;
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
   const int tile = pick_tile(layout, tiles64, splitk);
+  // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
+  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22) && glds_ok(a, nprob)) {
+    a.counters = counters;
+    do_reduce = false;
+  }
   if (do_main) switch (layout) {
     case SCA_GEMM_NT: rc = launch_tile<SCA_GEMM_NT>(tile, a, nprob, maxM, maxN, st); break;
     case SCA_GEMM_NN: rc = launch_tile<SCA_GEMM_NN>(tile, a, nprob, maxM, maxN, st); break;
@@ -1578,8 +1677,17 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   if (rc != SCA_OK) { sca_set_error("sca_gemm: launch failed"); return rc; }
   if (splitk > 1 && do_reduce) {
     const long MN = (long)maxM * maxN;
-    dim3 grid((unsigned)((MN + maxM + 255) / 256), nprob);
-    hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, a, nprob);
+    bool vec = true;  // 16-B form: every N and ldc a multiple of 4, C 16-byte aligned
+    for (int i = 0; i < nprob; ++i)
+      vec = vec && !(probs[i].N & 3) && !(probs[i].ldc & 3) && !(reinterpret_cast<uintptr_t>(probs[i].C) & 15);
+    if (vec) {
+      const int nc4 = (int)((MN / 4 + 255) / 256);
+      dim3 grid((unsigned)(nc4 + (maxM + 255) / 256), nprob);
+      hipLaunchKernelGGL(splitk_reduce4_kernel, grid, dim3(256), 0, st, a, nc4);
+    } else {
+      dim3 grid((unsigned)((MN + maxM + 255) / 256), nprob);
+      hipLaunchKernelGGL(splitk_reduce_kernel, grid, dim3(256), 0, st, a, nprob);
+    }
     if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm: reduce launch failed"); return SCA_ERR_LAUNCH; }
   }
   return SCA_OK;
@@ -1599,6 +1707,15 @@ extern "C" int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* p
 extern "C" int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                                void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, false, true);
+}
+
+extern "C" long sca_gemm_splitk_counters(int nprob, int maxM, int maxN) {
+  return (long)nprob * ((maxM + GL_BM - 1) / GL_BM) * ((maxN + GL_BN - 1) / GL_BN);
+}
+
+extern "C" int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_problem* probs, int splitk,
+                                     float* workspace, unsigned* counters, void* stream) {
+  return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, true, counters);
 }
 
 extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,

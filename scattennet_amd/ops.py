@@ -173,6 +173,27 @@ def dropout_grouped(xs, p):
     return list(Dropout.apply(float(p), *xs))
 
 
+# split-K slabs combined inside the GEMM launch by the last-arriving split (sca_gemm_splitk_fused)
+_SPLITK_FUSED = __import__("os").environ.get("SCA_SPLITK_FUSED", "1") != "0"
+_CNT = None
+_CNT_POS = 0
+_CNT_SIZE = 1 << 16
+
+
+def _splitk_counters(n):
+    """n zeroed tile counters from a persistent ring (the kernel leaves them zero); launches
+    far enough apart to share a slot have long completed (a step uses < 32k)."""
+    global _CNT, _CNT_POS
+    if _CNT is None:
+        _CNT = torch.zeros(_CNT_SIZE, dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+    n = -(-n // 64) * 64
+    if _CNT_POS + n > _CNT_SIZE:
+        _CNT_POS = 0
+    t = _CNT[_CNT_POS:_CNT_POS + n]
+    _CNT_POS += n
+    return t
+
+
 def gemm(layout, probs, splitk=1, ws=None):
     lib = L.lib()
     st = L.stream_handle()
@@ -180,10 +201,17 @@ def gemm(layout, probs, splitk=1, ws=None):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
+        if splitk > 1 and _SPLITK_FUSED and "sca_gemm_splitk_fused" not in L.MISSING:
+            cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
+                                                                max(p.N for p in chunk)))
+            with _timed(_GEMM_NAMES[layout], flops):
+                L.check(lib.sca_gemm_splitk_fused(layout, len(chunk), arr, splitk, ptr(ws), ptr(cnt), st),
+                        "sca_gemm_splitk_fused")
+            continue
         with _timed(_GEMM_NAMES[layout], flops):
             L.check(lib.sca_gemm_partial(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm")
         if splitk > 1:  # the fixed-order slab reduction: its own launch (timed apart)
-            with _timed("splitk_reduce_kernel", 0.0):
+            with _timed("splitk_reduce4_kernel", 0.0):
                 L.check(lib.sca_gemm_reduce(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm_reduce")
 
 

@@ -140,12 +140,17 @@ def test_blocks_d256_vs_oracle(block, fused):
             assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("splitk", [1, 3, 4])
-def test_weight_gradient_gemm_mixed_shapes(splitk):
+def test_weight_gradient_gemm_mixed_shapes(splitk, fused, monkeypatch):
     """The TN (weight-gradient) split-K GEMM with problems of different shapes in one launch
-    (fc1 768x256 and fc2 256x768 weight gradients, bias colsums fused) vs float64."""
+    (fc1 768x256 and fc2 256x768 weight gradients, bias colsums fused) vs float64 — the slab
+    combine in the same launch (last arriver, sca_gemm_splitk_fused) and as a second launch;
+    repeated launches on the same counters (they must be left zero) and a ragged
+    (100 x 36, K = 1000) problem."""
     _need_gpu()
     from scattennet_amd import _lib as L, ops
+    monkeypatch.setattr(ops, "_SPLITK_FUSED", fused)
     dev = torch.device("cuda:0")
     torch.manual_seed(splitk)
     Mr = 2048
@@ -159,9 +164,24 @@ def test_weight_gradient_gemm_mixed_shapes(splitk):
         keep.append((dY, X, dW, db))
         wsz += splitk * (n_out * n_in + n_out)
     ws = torch.empty(wsz, device=dev) if splitk > 1 else None
-    ops.gemm(L.GEMM_TN, probs, splitk=splitk, ws=ws)
+    for _ in range(3):  # the same counters / workspace three times
+        for _, _, dW, db in keep:
+            dW.fill_(float("nan"))
+            db.fill_(float("nan"))
+        ops.gemm(L.GEMM_TN, probs, splitk=splitk, ws=ws)
+        torch.cuda.synchronize()
+        for dY, X, dW, db in keep:
+            ref = 0.5 * dY.double().cpu().T @ X.double().cpu()
+            assert rel_err(dW.cpu(), ref) < 1e-5
+            assert rel_err(db.cpu(), dY.double().cpu().sum(0)) < 1e-5
+    if fused and ops._CNT is not None:
+        assert int(ops._CNT.abs().sum()) == 0  # every tile counter reset by its last arriver
+    # a ragged problem: rows / columns not multiples of the 64x64 tile, uneven K chunks
+    dY, X = torch.randn(1000, 100, device=dev), torch.randn(1000, 36, device=dev)
+    dW, db = torch.empty(100, 36, device=dev), torch.empty(100, device=dev)
+    p = ops._prob([ops._seg(dY, X, 100, 36, 1000)], dW, 100, 36, 36, bias_grad=db)
+    ws2 = torch.empty(splitk * (100 * 36 + 100), device=dev) if splitk > 1 else None
+    ops.gemm(L.GEMM_TN, [p], splitk=splitk, ws=ws2)
     torch.cuda.synchronize()
-    for dY, X, dW, db in keep:
-        ref = 0.5 * dY.double().cpu().T @ X.double().cpu()
-        assert rel_err(dW.cpu(), ref) < 1e-5
-        assert rel_err(db.cpu(), dY.double().cpu().sum(0)) < 1e-5
+    assert rel_err(dW.cpu(), dY.double().cpu().T @ X.double().cpu()) < 1e-5
+    assert rel_err(db.cpu(), dY.double().cpu().sum(0)) < 1e-5
