@@ -156,7 +156,8 @@ int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_prob
  *        them with sca_reduce_rows over nblk = sca_gemm_lnb_blocks(M) rows)
  * Replaces the input-gradient GEMM of a post-LN block's first op (the attention block's
  * dX = dq Wq + dk Wk + dv Wv + dY, the FFN's dx = dz W1 + dY) followed by the separate
- * LayerNorm backward of the block below (keypoint_module.py:69-72, 105-109).
+ * LayerNorm backward of the block below (keypoint_module.py:69-72, 105-109), and, with
+ * `wo`, that block's out-projection input-gradient GEMM as well.
  * Requires N == 256, 1..3 segments with K a positive multiple of 32 and one alpha, B
  * k-major (B[k][n] at B + k*ldb + n), 16-byte aligned operands, leading dimensions
  * multiples of 4; else SCA_ERR_ARG.                                                       */
@@ -167,6 +168,12 @@ typedef struct {
   const float* gamma; /* [256] */
   float* dx;          /* [M, 256] gradient w.r.t. x */
   float* partial;     /* [2, nblk, 256] dgamma / dbeta partials */
+  /* optional chained GEMM (NULL = none): dout = dx Wo, Wo [256, 256] row-major (an
+   * nn.Linear weight [out, in]: dout is the gradient of the Linear's INPUT when dx is the
+   * gradient of its output) — the out-projection input gradient of the attention block that
+   * produced the LayerNorm input (attention.py:74 backwards), in the same launch           */
+  const float* wo;
+  float* dout;        /* [M, 256] */
 } sca_gemm_lnb_problem;
 
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);

@@ -1068,7 +1068,15 @@ constexpr int LB_BM = 32, LB_S = 3;
 constexpr int LB_BROW = 1056;                        // bytes per k-row of the B image
 constexpr int LB_A_BYTES = LB_BM * GL_BK * 4;        // 4 KiB
 constexpr int LB_STAGE = LB_A_BYTES + GL_BK * LB_BROW;
-constexpr int LB_RED_OFF = 40 * 1024;                // epilogue: V tile at 0, wave partials here
+// epilogue / chained-GEMM LDS map: [0, 2 B-rows stages) the V tile, then phase 2's B ring
+// (2 stages); then phase 2's A image (the dx tile, rows of 256 + 4 floats); then the
+// dgamma / dbeta wave partials
+constexpr int LB_B2 = GL_BK * LB_BROW;                // one phase-2 B stage (33 KB)
+constexpr int LB_A2_LD = 260;                         // floats per row of the dx tile image
+constexpr int LB_A2_OFF = 2 * LB_B2;
+constexpr int LB_RED_OFF = LB_A2_OFF + LB_BM * LB_A2_LD * 4;
+constexpr int LB_SMEM = LB_RED_OFF + 2 * 8 * 256 * 4 > LB_S * LB_STAGE ? LB_RED_OFF + 2 * 8 * 256 * 4
+                                                                         : LB_S * LB_STAGE;
 
 struct GemmLnbArgs {
   sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
@@ -1076,8 +1084,8 @@ struct GemmLnbArgs {
 };
 
 __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
-  __shared__ __attribute__((aligned(1024))) char smem[LB_S * LB_STAGE];
-  static_assert(LB_RED_OFF >= LB_BM * LG_VS * 4 && LB_RED_OFF + 2 * 8 * LG_BN * 4 <= LB_S * LB_STAGE, "LDS map");
+  __shared__ __attribute__((aligned(1024))) char smem[LB_SMEM];
+  static_assert(LB_B2 >= LB_BM * LG_VS * 4 && LB_RED_OFF + 2 * 8 * LG_BN * 4 <= LB_SMEM, "LDS map");
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
   const unsigned orig = blockIdx.x + gx * blockIdx.z;
@@ -1177,6 +1185,20 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     const f32x4 ggx = gg * xh[i];
     s2[i] = (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
   }
+  // chained GEMM (dout = dx Wo): its first two B slices stream in under the LayerNorm math,
+  // into the V tile's region once every wave has read its rows of it
+  const bool chain = LN.wo != nullptr;
+  const float* pw = LN.wo + (long)(4 * wave) * LG_BN + 4 * lane;  // B pieces: k-rows 4*wave .. +3
+  auto dma2 = [&](int t, int stage) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      gl_dma(pw + (long)(32 * t + c) * LG_BN, smem + stage * LB_B2 + (4 * wave + c) * LB_BROW);
+  };
+  if (chain) {
+    __syncthreads();
+    dma2(0, 0);
+    dma2(1, 1);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
@@ -1185,13 +1207,15 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
       s2[i] += __shfl_xor(s2[i], o, 64);
     }
   f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pbsum = {0.f, 0.f, 0.f, 0.f};
+  float* A2 = reinterpret_cast<float*>(smem + LB_A2_OFF);
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const int m = m0 + RPW * wave + i;
+    const int lr = RPW * wave + i, m = m0 + lr;
+    const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * LN.rstd[min(m, P.M - 1)];
+    if (chain) st4(A2 + lr * LB_A2_LD + n, d);  // rows past M: finite, their products never stored
     if (m < P.M) {
-      const float rstd = LN.rstd[m];
       st4(P.C + (long)m * P.ldc + n, g[i]);
-      st4(LN.dx + (long)m * LG_BN + n, (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rstd);
+      st4(LN.dx + (long)m * LG_BN + n, d);
       pg += g[i] * xh[i];
       pbsum += g[i];
     }
@@ -1207,6 +1231,41 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
                      ((rr[4 * LG_BN] + rr[5 * LG_BN]) + (rr[6 * LG_BN] + rr[7 * LG_BN])));
   const long nblk = (P.M + LB_BM - 1) / LB_BM;
   LN.partial[(which * nblk + bx) * LG_BN + c] = sum;
+  if (!chain) return;
+
+  // chained GEMM: dout[32 x 256] = dx_tile[32 x 256] Wo[256 x 256]; A from the LDS image
+  // (written above, published by the barrier), B through a 2-stage ring, one slice ahead
+  f32x16 acc2;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+  constexpr int NS2 = LG_BN / GL_BK;  // 8 slices
+  for (int t = 0; t < NS2; ++t) {
+    gl_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t >= 1 && t + 1 < NS2) dma2(t + 1, (t + 1) & 1);  // into the stage slice t-1 left
+    const float* Bf = reinterpret_cast<const float*>(smem + (t & 1) * LB_B2);
+    f32x4 fa[4], fb[4];
+#pragma unroll
+    for (int g2 = 0; g2 < 4; ++g2) {
+      fa[g2] = ld4(A2 + col * LB_A2_LD + 32 * t + 8 * g2 + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[g2][j] = Bf[(8 * g2 + 4 * h + j) * (LB_BROW / 4) + 32 * wave + col];
+    }
+#pragma unroll
+    for (int g2 = 0; g2 < 4; ++g2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc2 = mfma32(fa[g2][j], fb[g2][j], acc2);
+  }
+  __syncthreads();  // ring free: wave-private transposition scratch (8 x 5 KB) for row stores
+  f32x4 rows[4];
+  acc_to_rows(acc2, reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD, lane, rows);
+  const int n2 = 32 * wave + 4 * (lane & 7);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + (lane >> 3) + 8 * i;
+    if (m < P.M) st4(LN.dout + (long)m * LG_BN + n2, rows[i]);
+  }
 }
 
 // ------------------------------------------------------------------------------ persistent
@@ -1786,7 +1845,9 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
               (!P.resid || ((P.ldr & 3) == 0 && P.ldr >= LG_BN));
     uintptr_t al = reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
                    reinterpret_cast<uintptr_t>(L.x) | reinterpret_cast<uintptr_t>(L.gamma) |
-                   reinterpret_cast<uintptr_t>(L.dx);
+                   reinterpret_cast<uintptr_t>(L.dx) | reinterpret_cast<uintptr_t>(L.wo) |
+                   reinterpret_cast<uintptr_t>(L.dout);
+    ok = ok && ((L.wo == nullptr) == (L.dout == nullptr));
     for (int s = 0; ok && s < P.nseg; ++s) {
       const sca_gemm_seg& S = P.seg[s];
       ok = S.A && S.B && S.K >= GL_BK && S.K % GL_BK == 0 && (S.lda & 3) == 0 && S.lda >= S.K &&

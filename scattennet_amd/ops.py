@@ -250,11 +250,13 @@ class LnSaved:
     tensor (`y._sca_ln`) so that the op consuming y can run this LayerNorm's backward in
     its own input-gradient GEMM's epilogue (sca_gemm_lnb): the LN input v, its row mean /
     rstd and gamma.  `handoff` carries the result back to the producer's backward:
-    (dL/dy as the consumer returned it, its version, dL/dv, dgamma/dbeta partials, nblk)."""
-    __slots__ = ("v", "mean", "rstd", "gamma", "handoff")
+    (dL/dy as the consumer returned it, its version, dL/dv, dgamma/dbeta partials, nblk,
+    dout).  `wo`: the producer's out-projection weight when it is an attention block whose
+    next backward step is dO = dL/dv Wo (no dropout) — chained into the same launch, `dout`."""
+    __slots__ = ("v", "mean", "rstd", "gamma", "handoff", "wo")
 
-    def __init__(self, v, mean, rstd, gamma):
-        self.v, self.mean, self.rstd, self.gamma, self.handoff = v, mean, rstd, gamma, None
+    def __init__(self, v, mean, rstd, gamma, wo=None):
+        self.v, self.mean, self.rstd, self.gamma, self.handoff, self.wo = v, mean, rstd, gamma, None, wo
 
 
 def ln_saved_of(ts):
@@ -265,8 +267,12 @@ def ln_saved_of(ts):
     return out if all(o is not None for o in out) else None
 
 
-def _attach_ln_saved(ys, vs, means, rstds, gam):
-    objs = [LnSaved(vs[g], means[g], rstds[g], gam[g]) for g in range(len(ys))]
+_CHAIN_DO = __import__("os").environ.get("SCA_CHAIN_DO", "1") != "0"
+
+
+def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None):
+    objs = [LnSaved(vs[g], means[g], rstds[g], gam[g], wo[g] if (wo is not None and _CHAIN_DO) else None)
+            for g in range(len(ys))]
     for y, o in zip(ys, objs):
         y._sca_ln = o
     return objs
@@ -281,19 +287,24 @@ def gemm_lnb(probs, lnp):
     nblk = lib.sca_gemm_lnb_blocks(M)
     dv = [torch.empty_like(o.v) for o in lnp]
     part = [o.v.new_empty(2 * nblk * o.v.shape[-1]) for o in lnp]
+    chain = all(o.wo is not None for o in lnp)  # the producers' dO = dv Wo in the same launch
+    dout = [torch.empty_like(o.v) for o in lnp] if chain else [None] * len(lnp)
     arr = (L.GemmProblem * len(probs))(*probs)
     larr = (L.GemmLnbProblem * len(lnp))(*[L.GemmLnbProblem(o.v.data_ptr(), o.mean.data_ptr(), o.rstd.data_ptr(),
-                                                           o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr())
+                                                           o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr(),
+                                                           ptr(o.wo) if chain else None, ptr(dout[g]))
                                             for g, o in enumerate(lnp)])
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
+    if chain and _PROFILER:
+        flops += sum(2.0 * p.M * 256 * 256 for p in probs)
     with _timed("gemm_lnb_kernel", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
-    return dv, part, nblk
+    return dv, part, nblk, dout
 
 
-def hand_off(lnp, dxs, dv, part, nblk):
+def hand_off(lnp, dxs, dv, part, nblk, dout):
     for g, o in enumerate(lnp):
-        o.handoff = (dxs[g], dxs[g]._version, dv[g], part[g], nblk)
+        o.handoff = (dxs[g], dxs[g]._version, dv[g], part[g], nblk, dout[g])
 
 
 def _take_handoff(lnsaved, dys):
@@ -318,7 +329,7 @@ def _ln_bwd_or_handoff(dys, vs, gam, means, rstds, lnsaved, bet):
     params = tuple(gam) + tuple(bet)
     if hs is None:
         dys = _contig(_zeros_for_none(dys, vs))
-        return _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE, params=params)
+        return _ln_bwd(dys, vs, gam, means, rstds, defer_affine=_LN_AFFINE_SIDE, params=params) + (None,)
     G, N, nblk = len(gam), gam[0].shape[0], hs[0][4]
     dg = [param_grad_empty(t) for t in gam]
     db = [param_grad_empty(b) for b in bet]
@@ -332,7 +343,8 @@ def _ln_bwd_or_handoff(dys, vs, gam, means, rstds, lnsaved, bet):
         reduce()
         params_produced(params)
         finish = None
-    return [h[2] for h in hs], dg, db, finish
+    dout = [h[5] for h in hs] if all(h[5] is not None for h in hs) else None
+    return [h[2] for h in hs], dg, db, finish, dout
 
 
 def _ln_fwd_outputs(xs):
@@ -727,7 +739,7 @@ class AttentionBlock(Function):
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
-        ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam) if ln else None
+        ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, Wo if drop_p == 0 else None) if ln else None
         ctx.lnprev = lnprev if (lnprev is not None and d == 256 and has_resid) else None
         ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
                               *sm, *sl, *((*vs, *gam, *means, *rstds) if ln else ()))
@@ -754,10 +766,11 @@ class AttentionBlock(Function):
         av = 0.5 if cross else 1.0
         dgam = dbet = ()
         ln_finish = None
+        do = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             i += 6 * G
             vs, gam, means, rstds = (sv[i + j * G:i + (j + 1) * G] for j in range(4))
-            dys, dgam, dbet, ln_finish = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
+            dys, dgam, dbet, ln_finish, do = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
         else:
             dys = _contig(_zeros_for_none(dys, xq))
@@ -765,9 +778,10 @@ class AttentionBlock(Function):
         if ctx.drop_p > 0:
             dyo = [torch.empty_like(t) for t in dys]
             dropout_apply([(dys[g], dyo[g], ctx.seeds[g]) for g in range(G)], ctx.drop_p)
-        # out-projection: dO = dY' Wo
-        do = [torch.empty_like(t) for t in o]
-        gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
+        # out-projection: dO = dY' Wo (unless the consumer's sca_gemm_lnb already chained it)
+        if do is None:
+            do = [torch.empty_like(t) for t in o]
+            gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
         # dq comes back pre-multiplied by the q scale and dv by alpha_v, so that every GEMM below
         # runs with unit segment scales: dX = dq' Wq + dk Wk + dv' Wv, dWq = dq'^T x, ...
         dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do,
@@ -912,7 +926,7 @@ class FeedForwardResidual(Function):
         ln_finish = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             vs, gam, means, rstds = (sv[(5 + i) * G:(6 + i) * G] for i in range(4))
-            dys, dgam, dbet, ln_finish = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
+            dys, dgam, dbet, ln_finish, _ = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
         else:
             dys = _contig(_zeros_for_none(dys, x))

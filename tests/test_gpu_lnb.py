@@ -26,8 +26,9 @@ def _need_gpu():
         pytest.skip("needs a GPU")
 
 
+@pytest.mark.parametrize("chain", [False, True])
 @pytest.mark.parametrize("M,Ks", [(2048, (768,)), (2048, (256, 256, 256)), (1000, (256,)), (33, (32, 64))])
-def test_gemm_lnb_c_abi_vs_float64(M, Ks):
+def test_gemm_lnb_c_abi_vs_float64(M, Ks, chain):
     _need_gpu()
     from scattennet_amd import _lib as L, ops
     dev = torch.device("cuda:0")
@@ -50,8 +51,9 @@ def test_gemm_lnb_c_abi_vs_float64(M, Ks):
     nblk = L.lib().sca_gemm_lnb_blocks(M)
     part = torch.empty(2 * nblk * N, device=dev)
     prob = ops._prob(segs, C, M, N, N, resid=resid, ldr=N)
+    wo, dout = torch.randn(N, N, device=dev) / N ** 0.5, torch.full((M, N), float("nan"), device=dev)
     lnp = L.GemmLnbProblem(x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gam.data_ptr(), dx.data_ptr(),
-                           part.data_ptr())
+                           part.data_ptr(), wo.data_ptr() if chain else None, dout.data_ptr() if chain else None)
     arr, larr = (L.GemmProblem * 1)(prob), (L.GemmLnbProblem * 1)(lnp)
     L.check(L.lib().sca_gemm_lnb(1, arr, larr, L.stream_handle()), "sca_gemm_lnb")
     torch.cuda.synchronize()
@@ -66,6 +68,8 @@ def test_gemm_lnb_c_abi_vs_float64(M, Ks):
     pb = part[nblk * N:].view(nblk, N).sum(0).cpu()
     assert rel_err(pg, g64.grad) < 1e-4
     assert rel_err(pb, b64.grad) < 1e-4
+    if chain:  # the chained out-projection input gradient: dout = dx Wo
+        assert rel_err(dout.cpu(), x64.grad @ wo.double().cpu()) < 1e-4
 
 
 def test_gemm_lnb_rejects_bad_shapes():
