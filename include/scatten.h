@@ -134,13 +134,33 @@ int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_problem* probs, 
  * Requires nseg == 1, N == 256, K a positive multiple of 32, 16-byte aligned operands with
  * leading dimensions multiple of 4 (y has leading dimension 256), epi 0 or DROPOUT only;
  * else SCA_ERR_ARG (use sca_gemm + sca_layernorm_fwd).                                    */
+/* Optional chained NT GEMMs on the LayerNorm output y (same launch, the 32-row tile): pass p
+ * computes C_p = epi((y B_p^T + bias_p) * post_scale_p) for one 256-row block B_p of an
+ * nn.Linear weight ([256, 256] k-contiguous, row stride ldb), epi 0 or SCA_EPI_GELU (then
+ * aux_out receives the pre-activation) — the next op's projection (an FFN's fc1 = 3 passes,
+ * an attention block's q / k / v = 3 passes) without re-reading y or a launch boundary.    */
+typedef struct {
+  const float* B;
+  int ldb;
+  const float* bias; /* [256] or NULL */
+  float post_scale;
+  int epi;
+  float* C;
+  int ldc;
+  float* aux_out;
+  int ldo;
+} sca_gemm_chain_pass;
+
 typedef struct {
   const float* gamma; /* [N] */
   const float* beta;  /* [N] */
   float* y;           /* [M, N] */
   float* mean;        /* [M] */
   float* rstd;        /* [M] */
+  int npass;          /* 0..3 chained passes */
+  sca_gemm_chain_pass pass[3];
 } sca_gemm_ln_problem;
+#define SCA_GEMM_LN_MAX_PROBLEMS 8
 
 int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                 void* stream);

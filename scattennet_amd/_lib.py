@@ -17,6 +17,7 @@ c_u64 = ctypes.c_uint64
 
 GEMM_NT, GEMM_NN, GEMM_TN = 0, 1, 2
 EPI_GELU, EPI_DGELU, EPI_ACCUM, EPI_DROPOUT = 1, 2, 4, 8
+GEMM_LN_MAX_PROBLEMS = 8
 GEMM_MAX_PROBLEMS = 16
 ATTN_MAX_PROBLEMS = 8
 LN_MAX_PROBLEMS = 8
@@ -64,8 +65,14 @@ class LnBwdProblem(ctypes.Structure):
                 ("dgamma", c_void_p), ("dbeta", c_void_p), ("partial", c_void_p)]
 
 
+class ChainPass(ctypes.Structure):
+    _fields_ = [("B", c_void_p), ("ldb", c_int), ("bias", c_void_p), ("post_scale", c_float), ("epi", c_int),
+                ("C", c_void_p), ("ldc", c_int), ("aux_out", c_void_p), ("ldo", c_int)]
+
+
 class GemmLnProblem(ctypes.Structure):
-    _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("y", c_void_p), ("mean", c_void_p), ("rstd", c_void_p)]
+    _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("y", c_void_p), ("mean", c_void_p), ("rstd", c_void_p),
+                ("npass", c_int), ("passes", ChainPass * 3)]
 
 
 class GemmLnbProblem(ctypes.Structure):

@@ -868,9 +868,17 @@ struct LgCfg {
   static constexpr int BPW = 32 / NW;      // B pieces (8 rows of 32 k) per wave per slice
 };
 
+// chained passes (CH): LDS map after the main loop — [0, 64 KB) a 2-stage B ring (a pass's
+// [256][32] k-slice, the main loop's swizzled image), then the y tile (rows of 256 + 4
+// floats: the A operand of every pass), then 8 wave-private 5-KB transposition scratches
+constexpr int LG_A2_LD = 260;
+constexpr int LG_A2_OFF = 2 * LG_B_BYTES;
+constexpr int LG_SCR_OFF = LG_A2_OFF + 32 * LG_A2_LD * 4;
+constexpr int LG_CH_SMEM = LG_SCR_OFF + 8 * 32 * EPI_LD * 4;
+
 struct GemmLnArgs {
-  sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
-  sca_gemm_ln_problem ln[SCA_GEMM_MAX_PROBLEMS];
+  sca_gemm_problem p[SCA_GEMM_LN_MAX_PROBLEMS];
+  sca_gemm_ln_problem ln[SCA_GEMM_LN_MAX_PROBLEMS];
   float eps;
   const unsigned long long* drop_off;
 };
@@ -887,11 +895,32 @@ __device__ __forceinline__ f32x4 lg_slot(const char* img, int r, int slot) {
   return *(const f32x4*)(img + r * 128 + 16 * (slot ^ gl_swz(r)));
 }
 
-template <int BM>
+// one chained pass's epilogue on float4 row pieces: (acc + bias) * post_scale, GELU (keeps
+// the pre-activation) — epilogue_rows' order
+__device__ __forceinline__ void chain_rows(const sca_gemm_chain_pass& Q, const f32x4 (&v)[4], int mb, int M, int nb,
+                                           int lane) {
+  const int n = nb + 4 * (lane & 7);
+  const f32x4 bias = Q.bias ? ld4(Q.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mb + (lane >> 3) + 8 * i;
+    if (m >= M) continue;
+    f32x4 o = (v[i] + bias) * Q.post_scale;
+    if (Q.epi & SCA_EPI_GELU) {
+      st4(Q.aux_out + (long)m * Q.ldo + n, o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
+    }
+    st4(Q.C + (long)m * Q.ldc + n, o);
+  }
+}
+
+template <int BM, bool CH>
 __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmLnArgs args) {
   using CF = LgCfg<BM>;
   constexpr int S = CF::S;
-  __shared__ __attribute__((aligned(1024))) char smem[S * CF::STAGE];
+  static_assert(!CH || (BM == 32 && LG_CH_SMEM >= S * CF::STAGE && 32 * LG_VS * 4 <= LG_A2_OFF), "LDS map");
+  __shared__ __attribute__((aligned(1024))) char smem[CH ? LG_CH_SMEM : S * CF::STAGE];
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
   const unsigned orig = blockIdx.x + gx * blockIdx.z;
@@ -1020,6 +1049,23 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     if (P.resid) v[i] += ld4(P.resid + (long)m * P.ldr + n);
     s[i] = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   }
+  // chained passes: a slice of B (row r of the [256][32] image at r * 128 B, pieces 4w .. 4w+3
+  // by wave w) — the first two stream in under the LayerNorm math, into the V tile's region
+  // once every wave has read its rows of it
+  const int nsl = CH ? 8 * LN.npass : 0;
+  auto dma2 = [&](int u, int stage) {
+    const sca_gemm_chain_pass& Q = LN.pass[u >> 3];
+    char* base = smem + stage * LG_B_BYTES;
+    const long k0 = 32L * (u & 7);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      gl_dma(lg_src(Q.B, Q.ldb, 0, LG_BN, 4 * wave + c, lane) + k0, base + (4 * wave + c) * GL_PIECE);
+  };
+  if constexpr (CH) {
+    __syncthreads();
+    if (nsl > 0) dma2(0, 0);
+    if (nsl > 1) dma2(1, 1);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
@@ -1036,15 +1082,55 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     for (int i = 0; i < RPW; ++i) q[i] += __shfl_xor(q[i], o, 64);
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const int m = m0 + RPW * wave + i;
+    const int lr = RPW * wave + i, m = m0 + lr;
+    const float mean = s[i] * invN;
+    const float rstd = 1.0f / sqrtf(q[i] * invN + args.eps);
+    const f32x4 y = (v[i] - mean) * rstd * gam + bet;
+    if (CH) st4(reinterpret_cast<float*>(smem + LG_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
     if (m < P.M) {
-      const float mean = s[i] * invN;
-      const float rstd = 1.0f / sqrtf(q[i] * invN + args.eps);
       st4(P.C + (long)m * P.ldc + n, v[i]);
-      st4(LN.y + (long)m * LG_BN + n, (v[i] - mean) * rstd * gam + bet);
+      st4(LN.y + (long)m * LG_BN + n, y);
       if (lane == 0) {
         LN.mean[m] = mean;
         LN.rstd[m] = rstd;
+      }
+    }
+  }
+  if constexpr (CH) {
+    // chained NT GEMMs: out_p[32 x 256] = y_tile[32 x 256] B_p^T — A from the LDS image
+    // (published by the barrier below), B through the 2-stage ring one slice ahead;
+    // the passes are one continuous slice sequence (the next pass's first slice streams in
+    // under the current pass's last one)
+    const float* A2 = reinterpret_cast<const float*>(smem + LG_A2_OFF);
+    float* scratch = reinterpret_cast<float*>(smem + LG_SCR_OFF) + wave * 32 * EPI_LD;
+    const int col = lane & 31, h = lane >> 5;
+    f32x16 acc2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+    __syncthreads();  // every wave's y rows written to the image
+    for (int u = 0; u < nsl; ++u) {
+      gl_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
+      const int t = u & 7;
+      const char* Bs = smem + (u & 1) * LG_B_BYTES;
+      f32x4 fa[4], fb[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        fa[g] = ld4(A2 + col * LG_A2_LD + 32 * t + 8 * g + 4 * h);
+        fb[g] = gl_frag<true>(Bs, 32 * wave, g, lane);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc2 = mfma32(fa[g][j], fb[g][j], acc2);
+      if (t == 7) {
+        f32x4 rows[4];
+        acc_to_rows(acc2, scratch, lane, rows);
+        chain_rows(LN.pass[u >> 3], rows, m0, P.M, 32 * wave, lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
       }
     }
   }
@@ -1780,11 +1866,12 @@ extern "C" int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_probl
 extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                            void* stream) {
   if (nprob <= 0) return SCA_OK;
-  if (nprob > SCA_GEMM_MAX_PROBLEMS || !probs || !ln || !(eps >= 0.f)) {
+  if (nprob > SCA_GEMM_LN_MAX_PROBLEMS || !probs || !ln || !(eps >= 0.f)) {
     sca_set_error("sca_gemm_ln: bad nprob / pointers / eps");
     return SCA_ERR_ARG;
   }
   GemmLnArgs a;
+  bool chain = false;
   a.eps = eps;
   a.drop_off = sca_drop_offset_ptr();
   int maxM = 0;
@@ -1804,6 +1891,23 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
                     "operands with leading dimensions multiple of 4, and no epilogue other than dropout");
       return SCA_ERR_ARG;
     }
+    if (L.npass < 0 || L.npass > 3) {
+      sca_set_error("sca_gemm_ln: npass must be 0..3");
+      return SCA_ERR_ARG;
+    }
+    for (int q = 0; q < L.npass; ++q) {
+      const sca_gemm_chain_pass& Q = L.pass[q];
+      const bool gelu = Q.epi == SCA_EPI_GELU;
+      if (!Q.B || !Q.C || (Q.ldb & 3) || Q.ldb < LG_BN || (Q.ldc & 3) || Q.ldc < LG_BN ||
+          (Q.epi != 0 && !gelu) || (gelu && (!Q.aux_out || (Q.ldo & 3) || Q.ldo < LG_BN)) ||
+          ((reinterpret_cast<uintptr_t>(Q.B) | reinterpret_cast<uintptr_t>(Q.C) |
+            reinterpret_cast<uintptr_t>(Q.bias) | reinterpret_cast<uintptr_t>(gelu ? Q.aux_out : nullptr)) & 15)) {
+        sca_set_error("sca_gemm_ln: chained pass needs B [256, ldb >= 256] and C (ldc >= 256), 16-byte aligned, "
+                      "leading dimensions multiple of 4, epi 0 or SCA_EPI_GELU (with aux_out)");
+        return SCA_ERR_ARG;
+      }
+    }
+    chain = chain || L.npass > 0;
     a.p[i] = P;
     a.ln[i] = L;
     maxM = maxM > P.M ? maxM : P.M;
@@ -1814,12 +1918,15 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
   // K = 256 19.8 vs 20.8 us; 1x(2048,256,256): 15.2 vs 10.9 us
   static const int bm_env = getenv("SCA_GEMM_LN_BM") ? atoi(getenv("SCA_GEMM_LN_BM")) : 0;
   const long wg32 = (long)nprob * ((maxM + 31) / 32);
-  const int bm = bm_env ? bm_env : (wg32 >= 256 ? 32 : 16);
+  // (chained passes: always the 32-row tile)
+  const int bm = chain ? 32 : bm_env ? bm_env : (wg32 >= 256 ? 32 : 16);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (bm == 16) {
-    hipLaunchKernelGGL(gemm_ln_kernel<GL_A16>, dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
+  if (chain) {
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+  } else if (bm == 16) {
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A16, false>), dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(gemm_ln_kernel<GL_A32>, dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;

@@ -11,7 +11,7 @@ from torch import nn
 from . import ops
 from .attention import CrossAttention, SelfAttention, SelfCausalAttention, attention_grouped
 from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, coordinate_mapping_grouped, drop_p,
-                     ffn_grouped, pos_embed_layernorm_grouped)
+                     fc1_request, ffn_grouped, pos_embed_layernorm_grouped)
 from .residual import ResidualNetwork, residual_network_grouped
 from .utils import key_padding_mask
 
@@ -43,15 +43,31 @@ class CoordinateAttention(nn.Module):
         return coordinate_attention_grouped([self], [coord_embed], attention_mask)[0]
 
 
-def coordinate_attention_grouped(blocks, xs, mask):
+def coordinate_attention_grouped(blocks, xs, mask, nxt=None):
     """h = LN(x + Attn(x)); self type: h = LN(h + FFN(h))  (keypoint_module.py:61-80).
-    The residual adds ride in the out-projection / fc2 epilogues."""
+    The residual adds ride in the out-projection / fc2 epilogues; the FFN's fc1 is chained
+    into the out-projection launch, and `nxt` (the next block's q / k / v, qkv_request) into
+    the block's last launch."""
     kind = "self" if blocks[0].attn_type == "self_attn" else "causal"
     h = attention_grouped([b.attn for b in blocks], kind, xs, None, mask, resid=True, drop_p=drop_p(blocks),
-                          ln=[b.attn_layer_norm for b in blocks])
+                          ln=[b.attn_layer_norm for b in blocks],
+                          nxt=fc1_request([b.mlp for b in blocks]) if kind == "self" else nxt)
     if kind == "self":
-        h = ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks])
+        h = ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks], nxt=nxt)
     return h
+
+
+def qkv_request(blocks):
+    """ops.NextProjections for the q / k / v projections of self / causal attention blocks
+    (q carries the 1/sqrt(head_dim) scale, as AttentionBlock computes it)."""
+    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "fc1":
+        return None
+    specs = []
+    for b in blocks:
+        a = b.attn
+        Wq, bq, Wk, bk, Wv, bv = a.qkv_params()
+        specs.append([(Wq, bq, a.scaling, False), (Wk, bk, 1.0, False), (Wv, bv, 1.0, False)])
+    return ops.NextProjections(specs) if ops.NextProjections.eligible(specs) else None
 
 
 # --------------------------------------------------------------------------- A10
@@ -71,10 +87,10 @@ class CoordinatesMerge(nn.Module):
         return coordinates_merge_grouped([self], [y_embed], [x_embed], cross_attn_mask)[0]
 
 
-def coordinates_merge_grouped(blocks, ys, xs, mask):
+def coordinates_merge_grouped(blocks, ys, xs, mask, nxt=None):
     h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True, drop_p=drop_p(blocks),
-                          ln=[b.attn_layer_norm for b in blocks])
-    return ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks])
+                          ln=[b.attn_layer_norm for b in blocks], nxt=fc1_request([b.mlp for b in blocks]))
+    return ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks], nxt=nxt)
 
 
 # --------------------------------------------------------------------------- A11
@@ -138,11 +154,9 @@ def sca_grouped(scas, xs, ys, attention_mask):
         for t in list(se) + [self_mask.key_valid]:
             t.record_stream(branch)
         with torch.cuda.stream(branch):
-            for i in range(L):
-                s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, self_mask)
+            s = _self_stack(scas, s, self_mask, L)
     else:
-        for i in range(L):
-            s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, self_mask)
+        s = _self_stack(scas, s, self_mask, L)
     c = ce
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
@@ -150,8 +164,16 @@ def sca_grouped(scas, xs, ys, attention_mask):
             main.wait_stream(branch)
             for t in s:
                 t.record_stream(main)
-        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask)
+        nxt = qkv_request([m.causal_attn_layers[i + 1] for m in scas]) if i + 1 < L else None
+        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask, nxt=nxt)
     return c, s
+
+
+def _self_stack(scas, s, mask, L):
+    for i in range(L):
+        nxt = qkv_request([m.self_attn_layers[i + 1] for m in scas]) if i + 1 < L else None
+        s = coordinate_attention_grouped([m.self_attn_layers[i] for m in scas], s, mask, nxt=nxt)
+    return s
 
 
 _BRANCH_OVERLAP = __import__("os").environ.get("SCA_BRANCH_OVERLAP", "1") != "0"

@@ -47,17 +47,19 @@ def drop_p(mods, attr="dropout"):
     return p
 
 
-def ffn_grouped(ffns, xs, residual=True, ln=None):
+def ffn_grouped(ffns, xs, residual=True, ln=None, nxt=None):
     """G-way FFN (layers.py:104-108); with `residual` the enclosing block's residual add is
     fused (y = FFN(x) + x, keypoint_module.py:71-72 / :108-109); `ln` (G nn.LayerNorms): the
-    block's last LayerNorm, fused into the fc2 launch when d_model = 256."""
+    block's last LayerNorm, fused into the fc2 launch when d_model = 256; `nxt`
+    (ops.NextProjections): the next op's projections, chained into that launch when fused."""
     G = len(xs)
     ts = [*xs, *[f.fc1.weight for f in ffns], *[f.fc1.bias for f in ffns], *[f.fc2.weight for f in ffns],
           *[f.fc2.bias for f in ffns]]
     fuse = ln is not None and ops.ln_fusable(xs[0].shape[-1], ffns[0].fc2.weight.shape[1])
     if fuse:
         ts += [n.weight for n in ln] + [n.bias for n in ln]
-    out = list(ops.FeedForwardResidual.apply(G, residual, drop_p(ffns), float(ln[0].eps) if fuse else None, *ts))
+    out = list(ops.FeedForwardResidual.apply(G, residual, drop_p(ffns), float(ln[0].eps) if fuse else None,
+                                             nxt if fuse else None, *ts))
     if ln is not None and not fuse:
         out = layernorm_grouped(ln, out)
     return out
@@ -75,6 +77,16 @@ class FeedForward(nn.Module):
 
     def forward(self, x):
         return ffn_grouped([self], [x], residual=False)[0]
+
+
+def fc1_request(ffns):
+    """ops.NextProjections for the FFNs' fc1 (bias + GELU, keeping the pre-activation),
+    computed in the launch that produces their input; None when not applicable (dropout
+    inside the FFN, widths other than d_model = 256 / d_ff <= 768, SCA_CHAIN_NEXT=0)."""
+    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "qkv" or drop_p(ffns) > 0:
+        return None
+    specs = [[(f.fc1.weight, f.fc1.bias, 1.0, True)] for f in ffns]
+    return ops.NextProjections(specs) if ops.NextProjections.eligible(specs) else None
 
 
 def coordinate_mapping_grouped(maps, keypoints, joint_idx):

@@ -230,15 +230,17 @@ def gemm_ln(probs, lns, eps):
     """probs: NT sca_gemm problems (C receives the LayerNorm input v); lns: GemmLnProblem."""
     lib = L.lib()
     st = L.stream_handle()
-    for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
-        chunk, lchunk = probs[i:i + L.GEMM_MAX_PROBLEMS], lns[i:i + L.GEMM_MAX_PROBLEMS]
+    for i in range(0, len(probs), L.GEMM_LN_MAX_PROBLEMS):
+        chunk, lchunk = probs[i:i + L.GEMM_LN_MAX_PROBLEMS], lns[i:i + L.GEMM_LN_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
         larr = (L.GemmLnProblem * len(lchunk))(*lchunk)
-        flops = sum(2.0 * p.M * p.N * p.seg[0].K for p in chunk) if _PROFILER else 0.0
-        # the row-tile variant sca_gemm_ln picks (gemm.hip), for the kernel name rocprofv3 shows
-        bm = int(__import__("os").environ.get("SCA_GEMM_LN_BM", "0")) or (
+        flops = sum(2.0 * p.M * p.N * (p.seg[0].K + 256 * ln.npass) for p, ln in zip(chunk, lchunk)) \
+            if _PROFILER else 0.0
+        # the variant sca_gemm_ln picks (gemm.hip), for the kernel name rocprofv3 shows
+        chain = any(ln.npass > 0 for ln in lchunk)
+        bm = 32 if chain else int(__import__("os").environ.get("SCA_GEMM_LN_BM", "0")) or (
             32 if len(chunk) * ((max(p.M for p in chunk) + 31) // 32) >= 256 else 16)
-        with _timed(f"gemm_ln_kernel<{bm}>", flops):
+        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}>", flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
@@ -276,6 +278,86 @@ def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None):
     for y, o in zip(ys, objs):
         y._sca_ln = o
     return objs
+
+
+_CHAIN_NEXT = __import__("os").environ.get("SCA_CHAIN_NEXT", "1") != "0"
+_CHAIN_WHICH = __import__("os").environ.get("SCA_CHAIN_NEXT", "1")  # "fc1" / "qkv": one kind only (A/B)
+
+
+class NextProjections:
+    """A request to compute the NEXT op's input projections inside a fused GEMM + LayerNorm
+    launch (sca_gemm_ln's chained passes): y = LN(v) of the 32-row tile is still in LDS, so
+    out_j = epi((y W_j^T + b_j) * s_j) costs no y re-read and no launch of its own.  Made by
+    the caller that knows which op reads y next (keypoint_module: a block's FFN fc1, the next
+    block's q / k / v); the producer op fills it (`passes`), the consumer op takes the
+    results (`take`) only if it runs with exactly the requested, unmodified parameters on the
+    unmodified y — otherwise it computes its projections itself.
+
+    specs[g]: [(W [n, 256] contiguous, b or None, post_scale, gelu)], sum(n) <= 768, n % 256 == 0."""
+
+    def __init__(self, specs):
+        self.specs = specs
+        self.vers = [[(W._version, None if b is None else b._version) for W, b, _, _ in s] for s in specs]
+        self.outs = [None] * len(specs)
+        self.ys = [None] * len(specs)
+
+    @staticmethod
+    def eligible(specs):
+        for s in specs:
+            if sum(W.shape[0] for W, _, _, _ in s) > 256 * 3:
+                return False
+            for W, b, _, _ in s:
+                if (W.dim() != 2 or W.shape[1] != 256 or W.shape[0] % 256 or not W.is_contiguous() or
+                        (b is not None and not b.is_contiguous())):
+                    return False
+        return True
+
+    def passes(self, g, M, like):
+        """Producer: the ChainPass list of stream g (outputs allocated here)."""
+        ps, outs = [], []
+        for W, b, scale, gelu in self.specs[g]:
+            n = W.shape[0]
+            C = like.new_empty(M, n)
+            A = like.new_empty(M, n) if gelu else None
+            for p in range(n // 256):
+                ps.append(L.ChainPass(W[256 * p:].data_ptr(), W.stride(0),
+                                      b[256 * p:].data_ptr() if b is not None else None, float(scale),
+                                      L.EPI_GELU if gelu else 0, C[:, 256 * p:].data_ptr(), n,
+                                      A[:, 256 * p:].data_ptr() if gelu else None, n if gelu else 0))
+            outs.append((C, A))
+        self.outs[g] = outs
+        return ps
+
+    def attach(self, ys):
+        for g, y in enumerate(ys):
+            if self.outs[g] is not None:
+                y._sca_next = self
+                self.ys[g] = (y._version, y.data_ptr())
+
+    def take(self, g, y, params):
+        """Consumer: [(C, aux)] for stream g if `params` [(W, b)] are the requested ones."""
+        if self.outs[g] is None or self.ys[g] != (y._version, y.data_ptr()) or len(params) != len(self.specs[g]):
+            return None
+        for (W, b), (W0, b0, _, _), (wv, bv) in zip(params, self.specs[g], self.vers[g]):
+            if W is not W0 or b is not b0 or W._version != wv or (b is not None and b._version != bv):
+                return None
+        out, self.outs[g] = self.outs[g], None  # one consumer
+        return out
+
+
+def _next_of(xs):
+    return [getattr(x, "_sca_next", None) for x in xs]
+
+
+def _chain_lns(nxt, G, M, like, gam, bet, ys, means, rstds):
+    """GemmLnProblems of a fused GEMM + LayerNorm launch, with `nxt`'s chained passes."""
+    lns = []
+    for g in range(G):
+        ps = nxt.passes(g, M, like) if nxt is not None else []
+        arr = (L.ChainPass * 3)(*(ps + [L.ChainPass()] * (3 - len(ps))))
+        lns.append(L.GemmLnProblem(gam[g].data_ptr(), bet[g].data_ptr(), ys[g].data_ptr(), means[g].data_ptr(),
+                                   rstds[g].data_ptr(), len(ps), arr))
+    return lns
 
 
 def gemm_lnb(probs, lnp):
@@ -692,7 +774,7 @@ class AttentionBlock(Function):
     into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, *ts):
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, *ts):
         cross = kind == "cross"
         ln = ln_eps is not None  # post-LN LayerNorm fused into the out-projection (sca_gemm_ln)
         if ln:
@@ -710,16 +792,28 @@ class AttentionBlock(Function):
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
         q, k, v, probs = [], [], [], []
-        for g in range(G):
-            Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
-            xf, kf = _flat(xq[g]), _flat(xkv[g])
-            q.append(xq[g].new_empty(B, T, d))
-            k.append(xq[g].new_empty(B, Tk, d))
-            v.append(xq[g].new_empty(B, Tk, d))
-            probs.append(_prob([_seg(xf, Wq, d, d, d)], q[g], B * T, d, d, bias=bq, post_scale=scale))
-            probs.append(_prob([_seg(kf, Wk, d, d, d)], k[g], B * Tk, d, d, bias=bk))
-            probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
-        gemm(L.GEMM_NT, probs)
+        pre = None
+        if not cross:  # q / k / v computed by the producer of x (chained passes of its launch)
+            pre = [n.take(g, ts[g], [(W[6 * g], W[6 * g + 1]), (W[6 * g + 2], W[6 * g + 3]),
+                                     (W[6 * g + 4], W[6 * g + 5])]) if n is not None and ts[g] is xq[g] else None
+                   for g, n in enumerate(_next_of(ts[:G]))]
+            if any(p is None for p in pre):
+                pre = None
+        if pre is not None:
+            q = [p[0][0].view(B, T, d) for p in pre]
+            k = [p[1][0].view(B, T, d) for p in pre]
+            v = [p[2][0].view(B, T, d) for p in pre]
+        else:
+            for g in range(G):
+                Wq, bq, Wk, bk, Wv, bv = W[6 * g:6 * g + 6]
+                xf, kf = _flat(xq[g]), _flat(xkv[g])
+                q.append(xq[g].new_empty(B, T, d))
+                k.append(xq[g].new_empty(B, Tk, d))
+                v.append(xq[g].new_empty(B, Tk, d))
+                probs.append(_prob([_seg(xf, Wq, d, d, d)], q[g], B * T, d, d, bias=bq, post_scale=scale))
+                probs.append(_prob([_seg(kf, Wk, d, d, d)], k[g], B * Tk, d, d, bias=bk))
+                probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
+            gemm(L.GEMM_NT, probs)
         o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v)
         # v = x + dropout(o Wo^T + bo)  (keypoint_module.py:63-65 / :99-101) in one epilogue,
         # and with `ln` the block's LayerNorm y = LN(v) in the same launch
@@ -732,8 +826,9 @@ class AttentionBlock(Function):
                        resid=_flat(xq[g]) if has_resid else None, ldr=d,
                        drop=(seeds[g], drop_p) if drop_p > 0 else None) for g in range(G)]
         if ln:
-            gemm_ln(probs, [L.GemmLnProblem(gam[g].data_ptr(), bet[g].data_ptr(), ys[g].data_ptr(),
-                                            means[g].data_ptr(), rstds[g].data_ptr()) for g in range(G)], ln_eps)
+            gemm_ln(probs, _chain_lns(nxt, G, B * T, xq[0], gam, bet, ys, means, rstds), ln_eps)
+            if nxt is not None:
+                nxt.attach(ys)
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
@@ -824,7 +919,7 @@ class AttentionBlock(Function):
                 dW += list(wg[4 * g + j])
             dWo.append(wg[4 * g + 3][0])
             dbo.append(wg[4 * g + 3][1])
-        return (None,) * 10 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
+        return (None,) * 11 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
             tuple(dbo) + dgam + dbet
 
 
@@ -879,7 +974,7 @@ class FeedForwardResidual(Function):
     backward's dX GEMM of fc2 applies GELU' in its epilogue."""
 
     @staticmethod
-    def forward(ctx, G, has_r, drop_p, ln_eps, *ts):
+    def forward(ctx, G, has_r, drop_p, ln_eps, nxt, *ts):
         lnprev = ln_saved_of(ts[:G])  # the input came out of a fused GEMM + LayerNorm
         x = _contig(ts[:G])
         W1, b1, W2, b2 = ts[G:2 * G], ts[2 * G:3 * G], ts[3 * G:4 * G], ts[4 * G:5 * G]
@@ -890,14 +985,24 @@ class FeedForwardResidual(Function):
         B, T, d = x[0].shape
         M = B * T
         F_ = W1[0].shape[0]
-        zs = [x[0].new_empty(M, F_) for _ in range(G)]
-        acts = [x[0].new_empty(M, F_) for _ in range(G)]
         # layers.py:104-107: dropout(GELU(fc1 x)) -> fc2 -> dropout (+ x), each dropout fused
         s1 = dropout_seeds(G) if drop_p > 0 else [None] * G
         s2 = dropout_seeds(G) if drop_p > 0 else [None] * G
-        gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
-                               epi=L.EPI_GELU, aux_out=zs[g], ldo=F_,
-                               drop=(s1[g], drop_p) if drop_p > 0 else None) for g in range(G)])
+        pre = None
+        if drop_p == 0:  # fc1 computed by the producer of x (chained passes of its launch)
+            pre = [n.take(g, ts[g], [(W1[g], b1[g])]) if n is not None and ts[g] is x[g] else None
+                   for g, n in enumerate(_next_of(ts[:G]))]
+            if any(p is None for p in pre):
+                pre = None
+        if pre is not None:
+            acts = [p[0][0] for p in pre]
+            zs = [p[0][1] for p in pre]
+        else:
+            zs = [x[0].new_empty(M, F_) for _ in range(G)]
+            acts = [x[0].new_empty(M, F_) for _ in range(G)]
+            gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
+                                   epi=L.EPI_GELU, aux_out=zs[g], ldo=F_,
+                                   drop=(s1[g], drop_p) if drop_p > 0 else None) for g in range(G)])
         if ln:
             vs, ys, means, rstds = _ln_fwd_outputs(x)
         else:
@@ -906,8 +1011,9 @@ class FeedForwardResidual(Function):
                        resid=_flat(x[g]) if has_r else None, ldr=d,
                        drop=(s2[g], drop_p) if drop_p > 0 else None) for g in range(G)]
         if ln:
-            gemm_ln(probs, [L.GemmLnProblem(gam[g].data_ptr(), bet[g].data_ptr(), ys[g].data_ptr(),
-                                            means[g].data_ptr(), rstds[g].data_ptr()) for g in range(G)], ln_eps)
+            gemm_ln(probs, _chain_lns(nxt, G, M, x[0], gam, bet, ys, means, rstds), ln_eps)
+            if nxt is not None:
+                nxt.attach(ys)
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
@@ -958,7 +1064,7 @@ class FeedForwardResidual(Function):
         wg = weight_grads(items, extra=ln_finish)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
-        return (None, None, None, None) + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
+        return (None,) * 5 + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
             tuple(w for w, _ in dW2) + tuple(b for _, b in dW2) + dgam + dbet
 
 

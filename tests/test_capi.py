@@ -42,7 +42,7 @@ _STRUCTS = {  # C struct in include/scatten.h -> ctypes mirror in scattennet_amd
     "sca_gelu_bwd_problem": "GeluBwdProblem", "sca_reduce_problem": "ReduceProblem",
     "sca_coord_map_problem": "CoordMapProblem", "sca_coord_map_bwd_problem": "CoordMapBwdProblem",
     "sca_dropout_problem": "DropoutProblem", "sca_gemm_ln_problem": "GemmLnProblem",
-    "sca_gemm_lnb_problem": "GemmLnbProblem",
+    "sca_gemm_lnb_problem": "GemmLnbProblem", "sca_gemm_chain_pass": "ChainPass",
 }
 
 
@@ -59,7 +59,7 @@ def test_struct_layouts_match_header(tmp_path):
     for cs, py in _STRUCTS.items():
         lines.append(f'printf("{py} size %zu\\n", sizeof({cs}));')
         for f, _ in getattr(L, py)._fields_:
-            cf = {"inp": "in"}.get(f, f)  # C field names that are Python keywords
+            cf = {"inp": "in", "passes": "pass"}.get(f, f)  # C field names that are Python keywords
             lines.append(f'printf("{py}.{f} %zu\\n", offsetof({cs}, {cf}));')
     lines.append("return 0; }")
     src = tmp_path / "layout.c"

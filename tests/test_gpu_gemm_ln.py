@@ -74,6 +74,58 @@ def test_gemm_ln_grouped_row_tiles(K):
         assert rel_err(y.cpu(), y64) < 1e-4
 
 
+def _chain_pass(L, W, bias, C, scale, aux=None):
+    gelu = aux is not None
+    return L.ChainPass(W.data_ptr(), W.stride(0), bias.data_ptr() if bias is not None else None, scale,
+                       L.EPI_GELU if gelu else 0, C.data_ptr(), C.stride(0), aux.data_ptr() if gelu else None,
+                       aux.stride(0) if gelu else 0)
+
+
+@pytest.mark.parametrize("G,M,K,npass,gelu", [(4, 2048, 256, 3, True), (4, 2048, 768, 3, False),
+                                              (2, 1000, 256, 1, True), (1, 33, 32, 2, False)])
+def test_gemm_ln_chained_passes_vs_float64(G, M, K, npass, gelu):
+    """Chained NT passes on the LayerNorm output (an FFN's fc1 with GELU, or q / k / v)
+    written in the same launch: out_p = epi((y W_p^T + b_p) * s_p) from 256-row blocks of one
+    [256 * npass, 256] weight, against float64; ragged M, one to three passes."""
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    torch.manual_seed(G * M + K + npass)
+    N = 256
+    probs, lns, keep = [], [], []
+    for g in range(G):
+        A, W = torch.randn(M, K, device=dev), torch.randn(N, K, device=dev) / K ** 0.5
+        b, r = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
+        gam, bet = torch.randn(N, device=dev), torch.randn(N, device=dev)
+        v, y = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+        mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        W2, b2 = torch.randn(N * npass, N, device=dev) / N ** 0.5, torch.randn(N * npass, device=dev)
+        out = torch.full((M, N * npass), float("nan"), device=dev)
+        aux = torch.full((M, N * npass), float("nan"), device=dev) if gelu else None
+        scales = [0.25 * (p + 1) for p in range(npass)]
+        passes = [_chain_pass(L, W2[p * N:(p + 1) * N], b2[p * N:(p + 1) * N] if p != 1 else None,
+                              out[:, p * N:], scales[p], aux[:, p * N:] if gelu else None) for p in range(npass)]
+        passes += [L.ChainPass()] * (3 - npass)
+        probs.append(ops._prob([ops._seg(A, W, K, K, K)], v, M, N, N, bias=b, resid=r, ldr=N))
+        lns.append(L.GemmLnProblem(gam.data_ptr(), bet.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                   npass, (L.ChainPass * 3)(*passes)))
+        keep.append((A, W, b, r, gam, bet, v, y, W2, b2, out, aux, scales, mean, rstd))  # alive until it ran
+    ops.gemm_ln(probs, lns, 1e-5)
+    torch.cuda.synchronize()
+    for A, W, b, r, gam, bet, v, y, W2, b2, out, aux, scales, _, _ in keep:
+        v64 = r.double().cpu() + A.double().cpu() @ W.double().cpu().T + b.double().cpu()
+        y64 = torch.nn.functional.layer_norm(v64, (N,), gam.double().cpu(), bet.double().cpu(), 1e-5)
+        assert rel_err(v.cpu(), v64) < 1e-5
+        assert rel_err(y.cpu(), y64) < 1e-4
+        for p in range(npass):
+            bp = b2[p * N:(p + 1) * N].double().cpu() if p != 1 else 0.0
+            pre = (y64 @ W2[p * N:(p + 1) * N].double().cpu().T + bp) * scales[p]
+            want = torch.nn.functional.gelu(pre) if gelu else pre
+            assert rel_err(out[:, p * N:(p + 1) * N].cpu(), want) < 1e-4, p
+            if gelu:
+                assert rel_err(aux[:, p * N:(p + 1) * N].cpu(), pre) < 1e-4, p
+
+
 def test_gemm_ln_rejects_other_widths():
     _need_gpu()
     from scattennet_amd import _lib as L, ops
@@ -185,3 +237,51 @@ def test_weight_gradient_gemm_mixed_shapes(splitk, fused, monkeypatch):
     torch.cuda.synchronize()
     assert rel_err(dW.cpu(), dY.double().cpu().T @ X.double().cpu()) < 1e-5
     assert rel_err(db.cpu(), dY.double().cpu().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("chain", [True, False])
+def test_sca_stack_chained_projections_vs_oracle(chain, monkeypatch):
+    """A two-layer SeparativeCoordinateAttention at d_model 256 (keypoint_module.py:153-198)
+    with the next op's projections chained into each fused GEMM + LayerNorm launch (every
+    FFN's fc1; self layer 1's and causal layer 1's q / k / v) against the CPU oracle, forward
+    and every gradient; with the chain the forward issues 4 stand-alone NT GEMM launches
+    (self / causal layer 0 q/k/v, the two merges' q + k/v) instead of 10."""
+    _need_gpu()
+    import scattennet_amd as S
+    from scattennet_amd import _lib as L, ops
+    from scattennet_amd.workloads import model_cfg
+    monkeypatch.setattr(ops, "_CHAIN_NEXT", chain)
+    dev = torch.device("cuda:0")
+    torch.manual_seed(21)
+    B, T, d, H = 3, 80, 256, 16
+    cfg = model_cfg(d, H, 2, maxpos=T)
+    m = S.SeparativeCoordinateAttention(cfg)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn_like(p) / (p.shape[-1] ** 0.5 if p.dim() == 2 else 4.0))
+    m = m.to(dev)
+    x, y = torch.randn(B, T, d), torch.randn(B, T, d)
+    mask = torch.ones(B, T, dtype=torch.long)
+    mask[1, 50:] = 0
+    mask[2, 1:] = 0
+    xg, yg = x.to(dev).requires_grad_(True), y.to(dev).requires_grad_(True)
+    gout = torch.randn(B, T, d)
+    prof = ops.LaunchProfiler()
+    with prof:
+        out = m(xg, yg, mask.to(dev))
+    out.backward(gout.to(dev))
+    torch.cuda.synchronize()
+    nt = prof.stats().get(ops._GEMM_NAMES[L.GEMM_NT], {}).get("launches", 0)
+    assert nt == (4 if chain else 10), nt
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    xr, yr = x.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    ref = O.sca(p, "", xr, yr, mask, cfg)
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * gout).sum().backward()
+    assert rel_err(xg.grad, xr.grad) < PARITY_TOL
+    assert rel_err(yg.grad, yr.grad) < PARITY_TOL
+    gscale = max(float(v.grad.abs().max()) for v in p.values() if v.grad is not None)
+    named = dict(m.named_parameters())
+    for k, v in p.items():
+        if v.grad is not None:
+            assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))

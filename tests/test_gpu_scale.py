@@ -67,35 +67,65 @@ def _encoder_oracle(enc, cfg, kp, mask, gout):
     return ref.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}
 
 
-TIE_TOL = 1e-5  # |a - b| <= TIE_TOL * max(|a|, |b|, 0.1): below the fp32 forward error of either path
+DEV_TOL = 1e-4  # bound on the GPU / oracle forward deviation at the pool and ReLU inputs (relative)
+
+
+def _deviation(gpu, mine, where, stats):
+    """Measured forward deviation of the two implementations on this tensor (absolute), after
+    checking it is below DEV_TOL of the tensor's scale — ten times tighter than parity."""
+    scale = float(mine.abs().max().clamp_min(1e-6))
+    dev = float((gpu - mine)[where].abs().max()) if bool(where.any()) else 0.0
+    stats["max_rel_dev"] = max(stats["max_rel_dev"], dev / scale)
+    assert dev <= DEV_TOL * scale, (dev, scale)
+    return dev
 
 
 def _tie_aware_pool(o, gpu_in, stats):
     """MaxPool1d(2, 2) over frames of the oracle's (B, T, C) block output, choosing the element
-    the GPU chose wherever the pair is an fp32-level tie (which element wins such a pair is
-    decided by forward rounding, not by the algorithm) and the oracle's own argmax elsewhere
-    (first element on exact equality, as torch's MaxPool1d)."""
+    the GPU chose wherever the pair is a rounding tie — its two values closer than twice the
+    measured GPU / oracle deviation of this tensor, so that either order is consistent with
+    both computations — and the oracle's own argmax elsewhere (first element on exact
+    equality, as torch's MaxPool1d)."""
+    dev = _deviation(gpu_in, o.detach(), torch.ones_like(o, dtype=torch.bool), stats)
     a, b = o[:, 0::2], o[:, 1::2]
     ga, gb = gpu_in[:, 0::2], gpu_in[:, 1::2]
     mine, theirs = b > a, gb > ga
-    tie = (a - b).abs() <= TIE_TOL * torch.maximum(a.abs(), b.abs()).clamp(min=0.1)
+    tie = (a - b).abs() <= 2 * dev
     stats["ties"] += int((tie & (a != b)).sum())
     stats["flipped"] += int((tie & (mine != theirs)).sum())
     stats["disagree_outside_ties"] += int((~tie & (mine != theirs)).sum())
     return torch.where(torch.where(tie, theirs, mine), b, a)
 
 
+def _tie_aware_relu(z, gpu_out, stats):
+    """ReLU of the oracle's pre-activation z, passing (or blocking) the elements the GPU
+    passed (blocked) wherever z is zero to within twice the measured deviation (over the
+    elements both pass): which side of zero such an element lands on is decided by
+    rounding, not by the algorithm.  Elsewhere the oracle's own sign decides; the two must
+    agree."""
+    zd = z.detach()
+    mine, theirs = zd > 0, gpu_out > 0
+    dev = _deviation(gpu_out, zd, mine & theirs, stats)
+    tie = zd.abs() <= 2 * dev
+    stats["relu_ties"] += int((tie & (zd != 0)).sum())
+    stats["relu_flipped"] += int((tie & (mine != theirs)).sum())
+    stats["relu_disagree_outside_ties"] += int((~tie & (mine != theirs)).sum())
+    return torch.where(torch.where(tie, theirs, mine), z, torch.zeros_like(z))
+
+
 def test_cfg3_full_encoder_vs_oracle(monkeypatch):
     """BASELINE config 3: yaml model section, 3 streams + residual + fusion, ragged masks;
     output and EVERY gradient at the north-star 1e-3.
 
-    ReLU + MaxPool1d(2,2) make the gradient discontinuous at pairs whose two values are equal
-    to within fp32 forward rounding (at this seed e.g. right_encoder.residual.blocks.2 has
-    pairs 4e-6 apart at magnitude 6): which frame receives the gradient there is decided by
-    rounding in either implementation.  The oracle therefore pools such pairs (and only
-    those: |a - b| <= 1e-5 max(|a|, |b|, 0.1), detected and counted) the way the GPU did, from the
-    GPU's own pool inputs; outside them the two argmaxes must agree exactly.  No gradient
-    tolerance is relaxed."""
+    ReLU + MaxPool1d(2,2) make the gradient discontinuous at ReLU inputs that are zero, and at
+    pool pairs whose two values are equal, to within fp32 forward rounding (at this seed e.g.
+    right_encoder.residual.blocks.2 has pairs 4e-6 apart at magnitude 6): which element
+    receives the gradient there is decided by rounding in either implementation.  The oracle
+    therefore pools such pairs and passes such ReLU inputs — those closer (to each other / to
+    zero) than twice the two implementations' measured deviation on that tensor, which is
+    itself checked to be below 1e-4 of its scale; detected and counted — the way the GPU
+    did, from the GPU's own pool inputs / ReLU outputs; outside them the two decisions must
+    agree.  No gradient tolerance is relaxed."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     from scattennet_amd import ops
@@ -105,42 +135,61 @@ def test_cfg3_full_encoder_vs_oracle(monkeypatch):
     enc = W.build_encoder(w, dev, seed=4, init="random").eval()  # parity at eval (dropout off)
     kp, mask, gout = W.synthetic_batch(w, dev, seed=6, ragged=True)
     pool_inputs = []  # per downsampling block: [body, left, right] (the grouped launch order)
-    fwd = ops.MaxPoolT.forward
+    relu_outputs = []  # per residual block: norm1 -> ReLU, then norm2 + shortcut -> ReLU
+    fwd, lnfwd = ops.MaxPoolT.forward, ops.LayerNormAdd.forward
 
     def recording(ctx, G, *xs):
         pool_inputs.append([x.detach().cpu() for x in xs])
         return fwd(ctx, G, *xs)
 
+    def ln_recording(ctx, G, eps, pos_table, has_post, act, drop_p, *ts):
+        ys = lnfwd(ctx, G, eps, pos_table, has_post, act, drop_p, *ts)
+        if act:
+            relu_outputs.append([y.detach().cpu() for y in ys])
+        return ys
+
     monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(recording))
+    monkeypatch.setattr(ops.LayerNormAdd, "forward", staticmethod(ln_recording))
     fuse = enc(kp, mask)[0]
     fuse.backward(gout[0])
     torch.cuda.synchronize()
     monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(fwd))
+    monkeypatch.setattr(ops.LayerNormAdd, "forward", staticmethod(lnfwd))
     assert len(pool_inputs) == 2 and all(len(c) == 3 for c in pool_inputs)
 
     cfg = W.encoder_cfg(w)
-    order = iter([(s, c) for s in range(3) for c in range(2)])  # oracle: body, left, right; blocks 0, 2
-    stats = {"ties": 0, "flipped": 0, "disagree_outside_ties": 0}
-    block = O.residual_block
+    nblk = len(cfg["residual_blocks"])
+    assert len(relu_outputs) == 2 * nblk and all(len(c) == 3 for c in relu_outputs)
+    order = iter([(s, i) for s in range(3) for i in range(nblk)])  # oracle: body, left, right
+    stats = {"ties": 0, "flipped": 0, "disagree_outside_ties": 0,
+             "relu_ties": 0, "relu_flipped": 0, "relu_disagree_outside_ties": 0, "max_rel_dev": 0.0}
 
-    def residual_block(p, prefix, x, in_dim, out_dim, downsample):
-        o = block(p, prefix, x, in_dim, out_dim, False)
-        if not downsample:
-            return o
-        s, c = next(order)
-        return _tie_aware_pool(o, pool_inputs[c][s], stats)
+    def residual_block(p, prefix, x, in_dim, out_dim, downsample):  # O.residual_block, tie-aware
+        s, i = next(order)
+        r = O.linear(p, prefix + ".projection", x) if in_dim != out_dim else x
+        o = _tie_aware_relu(O.layer_norm(p, prefix + ".norm1", O.linear(p, prefix + ".linear1", x)),
+                            relu_outputs[2 * i][s], stats)
+        o = _tie_aware_relu(O.layer_norm(p, prefix + ".norm2", O.linear(p, prefix + ".linear2", o)) + r,
+                            relu_outputs[2 * i + 1][s], stats)
+        return _tie_aware_pool(o, pool_inputs[i // 2][s], stats) if downsample else o
 
     monkeypatch.setattr(O, "residual_block", residual_block)
     ref, grads = _encoder_oracle(enc, cfg, kp.cpu(), mask.cpu(), gout[0].cpu())
-    print(f"cfg3 max-pool pairs: {stats}")
-    assert stats["disagree_outside_ties"] == 0, stats
+    print(f"cfg3 max-pool pairs / ReLU inputs: {stats}")
+    assert stats["disagree_outside_ties"] == 0 and stats["relu_disagree_outside_ties"] == 0, stats
     assert rel_err(fuse, ref) < PARITY_TOL
     gscale = max(float(t.abs().max()) for t in grads.values())
     named = dict(enc.named_parameters())
+    bad, errs = [], []
     for k, gr in grads.items():
         assert named[k].grad is not None, k
         got = named[k].grad.cpu()
-        assert close(got, gr, PARITY_TOL, gscale), (k, rel_err(got, gr))
+        if not close(got, gr, PARITY_TOL, gscale):
+            bad.append(k)
+        if float(gr.abs().max()) >= 1e-4 * gscale:  # (not an analytically-zero gradient)
+            errs.append((round(rel_err(got, gr), 6), k))
+    print("cfg3 largest gradient errors:", sorted(errs, reverse=True)[:6])
+    assert not bad, bad
     for k, prm in named.items():  # parameters the reference never trains (long shortcuts)
         if k not in grads:
             assert prm.grad is None, k

@@ -41,8 +41,25 @@ def case(G, M, K, N=256):
                                                      0, 0, 0.0) for g in range(G)])
         L.check(L.lib().sca_layernorm_fwd(G, arr, M, N, M, 0, 1e-5, L.stream_handle()), "ln")
 
-    keep = (A, W, b, r, gam, bet, v, y, mean, rstd)
-    return dict(name=f"{G}x(M={M}, N={N}, K={K})", fused=fused, split=split, flops=2.0 * G * M * N * K, keep=keep)
+    # the next op's projection (fc1: 768 wide, bias + GELU) chained into the launch, vs the
+    # fused launch followed by a stand-alone NT GEMM
+    W1 = [torch.randn(768, N, device=dev) / N ** 0.5 for _ in range(G)]
+    b1 = [torch.randn(768, device=dev) for _ in range(G)]
+    z = [torch.empty(M, 768, device=dev) for _ in range(G)]
+    act = [torch.empty(M, 768, device=dev) for _ in range(G)]
+    nxt = ops.NextProjections([[(W1[g], b1[g], 1.0, True)] for g in range(G)])
+
+    def chained():
+        ops.gemm_ln(probs, ops._chain_lns(nxt, G, M, v[0], gam, bet, y, mean, rstd), 1e-5)
+
+    def unchained():
+        ops.gemm_ln(probs, lns, 1e-5)
+        ops.gemm(L.GEMM_NT, [ops._prob([ops._seg(y[g], W1[g], N, N, N)], act[g], M, 768, 768, bias=b1[g],
+                                       epi=L.EPI_GELU, aux_out=z[g], ldo=768) for g in range(G)])
+
+    keep = (A, W, b, r, gam, bet, v, y, mean, rstd, W1, b1, z, act)
+    return dict(name=f"{G}x(M={M}, N={N}, K={K})", fused=fused, split=split, flops=2.0 * G * M * N * K, keep=keep,
+                chained=chained, unchained=unchained, cflops=2.0 * G * M * N * (K + 768))
 
 
 def timed(fn, iters):
@@ -72,6 +89,11 @@ def main():
         tf, ts = timed(c["fused"], args.iters), timed(c["split"], args.iters)
         print(f"{c['name']:28s} fused {tf:7.2f} us ({c['flops'] / tf / 1e6:6.1f} TFLOP/s)   "
               f"gemm+ln {ts:7.2f} us")
+        c["chained"]()
+        torch.cuda.synchronize()
+        tc, tu = timed(c["chained"], args.iters), timed(c["unchained"], args.iters)
+        print(f"{'':28s} + fc1 chained {tc:7.2f} us ({c['cflops'] / tc / 1e6:6.1f} TFLOP/s)   "
+              f"fused + NT GEMM {tu:7.2f} us")
 
 
 if __name__ == "__main__":
