@@ -953,6 +953,16 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + CF::A_BYTES + (BPW * wave + c) * GL_PIECE);
   };
 
+  // the epilogue's residual rows are loaded before the main loop (their HBM reads overlap
+  // it); no residual: a harmless read of gamma, unused — keeps the loads branch-free
+  constexpr int RPW = BM / CF::NW;
+  const int n = 4 * lane;
+  f32x4 rin[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = min(m0 + RPW * wave + i, P.M - 1);
+    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
+  }
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = G.alpha;
   if constexpr (BM == 32) {
@@ -1027,8 +1037,6 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 
   // each wave normalises BM/NW rows at once: every row is 64 lanes x float4 (coalesced), and
   // the rows' reductions are interleaved (independent shuffle chains, one latency each)
-  constexpr int RPW = BM / CF::NW;
-  const int n = 4 * lane;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
   const f32x4 gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
@@ -1046,7 +1054,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[i][j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), v[i][j]);
     }
-    if (P.resid) v[i] += ld4(P.resid + (long)m * P.ldr + n);
+    if (P.resid) v[i] += rin[i];
     s[i] = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   }
   // chained passes: a slice of B (row r of the [256][32] image at r * 128 B, pieces 4w .. 4w+3
@@ -1214,6 +1222,22 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     for (int c = 0; c < 4; ++c) gl_dma(pb + (k0 + c) * ldb, base + LB_A_BYTES + (4 * wave + c) * LB_BROW);
   };
 
+  // the epilogue's row operands (this wave's 4 rows of the LayerNorm input, its statistics
+  // and the residual gradient) are loaded before the main loop: their HBM reads overlap it
+  // instead of forming the HBM-bound tail of every workgroup at once
+  constexpr int RPW = LB_BM / 8;
+  const int n = 4 * lane;
+  f32x4 xin[RPW], rin[RPW];
+  float mu[RPW], rs[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = min(m0 + RPW * wave + i, P.M - 1);
+    xin[i] = ld4(LN.x + (long)m * LG_BN + n);
+    // (no residual: a harmless read of gamma, unused — keeps the loads branch-free)
+    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
+    mu[i] = LN.mean[m];
+    rs[i] = LN.rstd[m];
+  }
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -1254,18 +1278,15 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
   __syncthreads();
 
-  constexpr int RPW = LB_BM / 8;
-  const int n = 4 * lane;
   const f32x4 gam = ld4(LN.gamma + n);
   const float invN = 1.0f / LG_BN;
   f32x4 g[RPW], xh[RPW];
   float s1[RPW], s2[RPW];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const int m = min(m0 + RPW * wave + i, P.M - 1);
     g[i] = ld4(&V[(RPW * wave + i) * LG_VS + n]);
-    if (P.resid) g[i] += ld4(P.resid + (long)m * P.ldr + n);
-    xh[i] = (ld4(LN.x + (long)m * LG_BN + n) - LN.mean[m]) * LN.rstd[m];
+    if (P.resid) g[i] += rin[i];
+    xh[i] = (xin[i] - mu[i]) * rs[i];
     const f32x4 gg = g[i] * gam;
     s1[i] = (gg[0] + gg[1]) + (gg[2] + gg[3]);
     const f32x4 ggx = gg * xh[i];
@@ -1297,7 +1318,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int lr = RPW * wave + i, m = m0 + lr;
-    const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * LN.rstd[min(m, P.M - 1)];
+    const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rs[i];
     if (chain) st4(A2 + lr * LB_A2_LD + n, d);  // rows past M: finite, their products never stored
     if (m < P.M) {
       st4(P.C + (long)m * P.ldc + n, g[i]);

@@ -16,10 +16,11 @@ from scattennet_amd import _lib as L, ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--sweep", action="store_true", help="K = 32 .. 1536 (one segment): fixed cost vs slope")
     a = ap.parse_args()
     dev = "cuda"
     M, N, G = 2048, 256, 4
-    for Ks in ((768,), (256, 256, 256)):
+    for Ks in (((32,), (256,), (512,), (768,), (1536,)) if a.sweep else ((768,), (256, 256, 256))):
         keep, probs, lnp = [], [], []
         for _ in range(G):
             segs = []
