@@ -127,7 +127,9 @@ def main():
         # thread-local capture mode with RCCL: ProcessGroupNCCL's watchdog thread queries the
         # warm-up steps' events while the step is captured (tools/dp_capture_diag.py)
         with torch.cuda.graph(graph, capture_error_mode="thread_local" if reducer is not None else "global"):
+            ops.fork_ledger_begin()  # every stream forked in the step must join the capture origin
             fwd_bwd()
+            ops.fork_ledger_end()
         for _ in range(2):
             graph.replay()
             sync()

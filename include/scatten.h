@@ -242,12 +242,17 @@ typedef struct {
   float* delta; /* workspace [B*H*Tq] : rowsum(dO * O) */
   float dq_scale;
   float dv_scale;
+  float* dq_part; /* workspace of sca_attn_bwd_workspace() floats, or NULL: with it (hd 32, no
+                     add_mask) the backward is one fused launch over 256-key blocks + a
+                     fixed-order dQ reduction; without it the split dq / dkdv kernels */
 } sca_attn_bwd_problem;
 
 #define SCA_ATTN_MAX_PROBLEMS 8
 
 int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B, int H, int Tq, int Tk, int hd,
                  int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream);
+/* dq_part floats per problem for the fused hd-32 backward (0 when that path does not apply) */
+long sca_attn_bwd_workspace(int B, int H, int Tq, int Tk, int hd);
 int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B, int H, int Tq, int Tk, int hd,
                  int ldq, int ldk, int ldv, int ldo, int causal, int plus_one, void* stream);
 /* Backward kernel choice: enable = 1 (default) runs the single-launch fused kernel where it

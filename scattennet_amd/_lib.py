@@ -50,7 +50,7 @@ class AttnBwdProblem(ctypes.Structure):
     _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("dout", c_void_p),
                 ("stat_m", c_void_p), ("stat_ll", c_void_p), ("key_valid", c_void_p), ("add_mask", c_void_p),
                 ("dq", c_void_p), ("dk", c_void_p), ("dv", c_void_p), ("delta", c_void_p), ("dq_scale", c_float),
-                ("dv_scale", c_float)]
+                ("dv_scale", c_float), ("dq_part", c_void_p)]
 
 
 class LnFwdProblem(ctypes.Structure):
@@ -123,6 +123,7 @@ EXPORTS = {
     "sca_gemm_lnb_blocks": ([c_int], c_int),
     "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
     "sca_attn_bwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
+    "sca_attn_bwd_workspace": ([c_int] * 5, ctypes.c_long),
     "sca_attn_bwd_fused": ([c_int], c_int),
     "sca_layernorm_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p], c_int),
     "sca_layernorm_bwd_blocks": ([c_int], c_int),

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
   for (int job = 0; job < jobs; ++job) {
   const int xb = job ? nqb - 1 - tid.x : tid.x;
   const int q0 = xb * QB;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int qi = lane & 15, grp = lane >> 4;
   const int qrow = q0 + 16 * w + qi;
   const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   for (int job = 0; job < jobs; ++job) {
   const int xb = job ? nqb - 1 - tid.x : tid.x;
   const int q0 = xb * QB;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int qi = lane & 15, grp = lane >> 4;
   const int qrow = q0 + 16 * w + qi;
   const bool qok = qrow < a.Tq;
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
 #pragma unroll 1
   for (int job = 0; job < jobs; ++job) {
   const int k0 = (job ? nkb - 1 - tid.x : tid.x) * KB;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int kj = lane & 15, grp = lane >> 4;
   const int krow = k0 + 16 * w + kj;
   const bool kok = krow < a.Tk;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
   const TileId tid = xcd_tile();
   const sca_attn_bwd_problem& P = a.p[tid.z];
   const int b = tid.y / a.H, h = tid.y % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int kj = lane & 15, grp = lane >> 4;
   const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
   const int Tq = a.Tq, Tk = a.Tk;
@@ -769,6 +769,277 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
   }
 }
 
+// ------------------------------------------------------------------------------ backward: fused, key blocks
+// Fused backward for hd 32 at any length (config 5: T = 1024, d = 512): one workgroup =
+// (problem, clip, head, 256-key block) — attn_bwd_fused_kernel's scheme (each wave owns
+// 16-key tiles with K, V, K^T in registers; S, P, dP, dS once per score; dV, dK accumulated
+// in registers; dS transposed through a wave-private LDS tile for dQ) with 8 waves of two
+// key tiles each (g = 8i + w: at hd 32 four tiles per wave would not fit 256 registers),
+// 32-query blocks, and dQ summed over the waves in fixed order and written as this key
+// block's PARTIAL; attn_dq_reduce_kernel adds the key blocks' partials in order
+// (deterministic, no atomics).  40 MFMAs per 16x16 score tile at hd 32 against the split
+// kernels' 56.  Causal: a key block sees only the queries at or after its first key.
+constexpr int KBLK = 256, QB2 = 32, KW = 8;
+
+// transposed image [HD][32 queries]: 4 consecutive queries at float4 slot `slot` (0..7) of
+// row d; rows 128 B apart, swizzled by (d >> 1) & 7 so that 16 rows d of one slot hit 16
+// distinct 16-B bank groups
+__device__ __forceinline__ f32x4 col_frag32(const float* img, int d, int slot) {
+  return ld4(img + d * QB2 + 4 * (slot ^ ((d >> 1) & 7)));
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs a) {
+  constexpr int HD = 32, NS = 8, ND = 2, TPW = KBLK / 16 / KW;
+  __shared__ __attribute__((aligned(16))) float Qs[2][QB2 * HD];
+  __shared__ __attribute__((aligned(16))) float Ds[2][QB2 * HD];
+  __shared__ __attribute__((aligned(16))) float Qt[2][HD * QB2];
+  __shared__ __attribute__((aligned(16))) float Dt[2][HD * QB2];
+  __shared__ __attribute__((aligned(16))) float Sm[2][QB2], Sl[2][QB2], Sd[2][QB2];
+  __shared__ __attribute__((aligned(16))) float dSw[KW][KBLK / 16 / KW][16 * FB_TS];
+  __shared__ __attribute__((aligned(16))) float dQr[KW][QB2 * HD];
+
+  // Dispatch order = blockIdx order (no XCD remap): x = (problem, clip, head), y = key block,
+  // so with the causal mask the heaviest workgroups (key block 0 sees every query) are
+  // dispatched first and the light ones fill in behind them (longest-first list scheduling;
+  // an interleaved order left the CUs that drew key block 0 running long after the rest).
+  // Consecutive workgroups still cycle over the 8 XCDs.
+  const int bh = blockIdx.x % (a.B * a.H), pz = blockIdx.x / (a.B * a.H);
+  const TileId tid{(int)blockIdx.y, bh, pz};
+  const sca_attn_bwd_problem& P = a.p[tid.z];
+  const int b = tid.y / a.H, h = tid.y % a.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  const int kj = lane & 15, grp = lane >> 4;
+  const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
+  const int Tq = a.Tq, Tk = a.Tk;
+  const int k0 = tid.x * KBLK;
+
+  // own key tiles g = KW i + w: K, V rows (lane (kj, grp): d = 8 grp .. 8 grp + 7) and the K^T
+  // fragments of both 16-wide d blocks (lane (d = 16 dd + kj, grp): K[16g + 4grp + r][d])
+  float kreg[TPW][NS], vreg[TPW][NS], kadd[TPW];
+  f32x4 ktf[TPW][ND];
+  const float* kb = P.k + (long)b * Tk * a.ldk + h * HD;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int key = k0 + 16 * (KW * i + w) + kj;
+    const int kc = min(key, Tk - 1);
+#pragma unroll
+    for (int s = 0; s < NS; s += 4) {
+      const f32x4 kv = ld4(kb + (long)kc * a.ldk + NS * grp + s);
+      const f32x4 vv = ld4(P.v + ((long)b * Tk + kc) * a.ldv + h * HD + NS * grp + s);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kreg[i][s + j] = kv[j];
+        vreg[i][s + j] = vv[j];
+      }
+    }
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ktf[i][dd][j] = kb[(long)min(k0 + 16 * (KW * i + w) + 4 * grp + j, Tk - 1) * a.ldk + 16 * dd + kj];
+    kadd[i] = key_add(kv_load(P.key_valid, b, key, Tk), false, key, Tk, plus2);
+  }
+  f32x4 dk[TPW][ND], dv[TPW][ND];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd) dk[i][dd] = dv[i][dd] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // query blocks: causal from the block holding this key block's first key (k0 % 32 == 0)
+  const int qbeg = CAUSAL ? k0 : 0;
+  const int nqb = qbeg < Tq ? (Tq - qbeg + QB2 - 1) / QB2 : 0;
+  const float* qbase = P.q + (long)b * Tq * a.ldq + h * HD;
+  const float* dbase = P.dout + (long)b * Tq * a.ldo + h * HD;
+  const float* obase = P.o + (long)b * Tq * a.ldo + h * HD;
+  // staging (waves 0-3): thread e owns row e / 8, float4 column (e % 8) of the 32 x 32 block
+  const bool stager = threadIdx.x < 256;
+  const int srow = (threadIdx.x & 255) >> 3, sc = 4 * (threadIdx.x & 7);
+  f32x4 rq, rd;
+  float cm = 0.f, cl = 0.f, cdel = 0.f;
+  int qbn = 0;
+  auto prefetch = [&](int q0) {
+    if (!stager) return;
+    const int q = min(q0 + srow, Tq - 1);
+    rq = ld4(qbase + (long)q * a.ldq + sc);
+    rd = ld4(dbase + (long)q * a.ldo + sc);
+    const f32x4 ro = ld4(obase + (long)q * a.ldo + sc);
+    // delta of row srow: 8 consecutive lanes hold its 32 dO*O products
+    float dp = rd[0] * ro[0] + rd[1] * ro[1] + rd[2] * ro[2] + rd[3] * ro[3];
+    dp += __shfl_xor(dp, 1, 64);
+    dp += __shfl_xor(dp, 2, 64);
+    dp += __shfl_xor(dp, 4, 64);
+    cdel = dp;
+    if (threadIdx.x < QB2) {
+      const int qq = q0 + threadIdx.x;
+      const long si = ((long)b * a.H + h) * Tq + min(qq, Tq - 1);
+      cm = P.stat_m[si];
+      cl = P.stat_ll[si];
+      if (qq >= Tq) cm = INFINITY;  // rows past the end: p = exp2(-inf) = 0
+    }
+    qbn = q0;
+  };
+  auto commit = [&](int buf) {
+    if (!stager) return;
+    st4(Qs[buf] + srow * HD + 4 * ((sc >> 2) ^ row_swz<HD>(srow)), rq);
+    st4(Ds[buf] + srow * HD + 4 * ((sc >> 2) ^ row_swz<HD>(srow)), rd);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = sc + j;
+      const int o = d * QB2 + 4 * ((srow >> 2) ^ ((d >> 1) & 7)) + (srow & 3);
+      Qt[buf][o] = rq[j];
+      Dt[buf][o] = rd[j];
+    }
+    if (threadIdx.x < QB2) {
+      Sm[buf][threadIdx.x] = cm;
+      Sl[buf][threadIdx.x] = cl;
+    }
+    if ((threadIdx.x & 7) == 0) {
+      Sd[buf][srow] = cdel;
+      if (k0 == 0 && qbn + srow < Tq) P.delta[((long)b * a.H + h) * Tq + qbn + srow] = cdel;
+    }
+  };
+  if (nqb > 0) {
+    prefetch(qbeg);
+    commit(0);
+  }
+  float* part = P.dq_part + ((long)tid.x * a.B + b) * Tq * (a.H * HD) + h * HD;
+
+  // one 16-query tile against the wave's key tiles; GEN: the general form (key tiles past Tk
+  // skipped, causal tiles after the query tile skipped, the diagonal one masked) — the
+  // blocks where every key tile is whole and (causal) before every query run the
+  // branch-free form, whose two key tiles' MFMA chains interleave
+  auto qtile = [&](auto gen_c, int buf, int q0, int t) {
+    constexpr bool GEN = decltype(gen_c)::value;
+    const int qt = (q0 >> 4) + t;  // global 16-query tile index
+    f32x4 qv[2], dov[2], dtf[ND], qtf[ND];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      qv[s2] = row_frag<HD>(Qs[buf], 16 * t + kj, 2 * grp + s2);
+      dov[s2] = row_frag<HD>(Ds[buf], 16 * t + kj, 2 * grp + s2);
+    }
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd) {
+      dtf[dd] = col_frag32(Dt[buf], 16 * dd + kj, 4 * t + grp);
+      qtf[dd] = col_frag32(Qt[buf], 16 * dd + kj, 4 * t + grp);
+    }
+    const int ql = 16 * t + 4 * grp;
+    const f32x4 sm = ld4(&Sm[buf][ql]), sl = ld4(&Sl[buf][ql]), sd = ld4(&Sd[buf][ql]);
+    f32x4 dq[ND];
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd) dq[dd] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int g = (k0 >> 4) + KW * i + w;  // global 16-key tile index
+      if (GEN && 16 * g >= Tk) continue;      // wave-uniform: no keys in this tile
+      if (GEN && CAUSAL && g > qt) continue;  // every key after every query of the tile
+      f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = s_acc;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s_acc = mfma16(qv[s2][j], kreg[i][4 * s2 + j], s_acc);
+          dp_acc = mfma16(dov[s2][j], vreg[i][4 * s2 + j], dp_acc);
+        }
+      float p[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t2 = fmaf(s_acc[r], L2E, kadd[i]);
+        if (GEN && CAUSAL && g == qt && kj > 4 * grp + r) t2 = -INFINITY;
+        p[r] = fast_exp2((t2 - sm[r]) - sl[r]);
+        ds[r] = p[r] * (dp_acc[r] - sd[r]);
+      }
+#pragma unroll
+      for (int dd = 0; dd < ND; ++dd)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dv[i][dd] = mfma16(dtf[dd][r], p[r], dv[i][dd]);
+          dk[i][dd] = mfma16(qtf[dd][r], ds[r], dk[i][dd]);
+        }
+      float* tw = dSw[w][i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tw[(4 * grp + r) * FB_TS + kj] = ds[r];
+    }
+    // dS^T through the wave-private tiles (one per key tile): one wave barrier for both
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int g = (k0 >> 4) + KW * i + w;
+      if (GEN && 16 * g >= Tk) continue;
+      if (GEN && CAUSAL && g > qt) continue;
+      const f32x4 dsv = ld4(&dSw[w][i][kj * FB_TS + 4 * grp]);
+#pragma unroll
+      for (int dd = 0; dd < ND; ++dd)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dq[dd] = mfma16(ktf[i][dd][r], dsv[r], dq[dd]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the tiles are rewritten
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // partial dQ^T[d = 16 dd + 4grp + r][q = 16t + kj] over this wave's keys
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd) st4(&dQr[w][(16 * t + kj) * HD + 16 * dd + 4 * grp], dq[dd]);
+  };
+
+#pragma unroll 1
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int buf = qb & 1;
+    const int q0 = qbeg + qb * QB2;
+    __syncthreads();  // block qb staged; the previous block's dQ partials consumed
+    if (qb + 1 < nqb) prefetch(q0 + QB2);  // in flight during this block
+    const bool full = k0 + KBLK <= Tk && (!CAUSAL || (q0 >> 4) >= (k0 >> 4) + KBLK / 16 - 1);
+    if (full) {
+#pragma unroll
+      for (int t = 0; t < QB2 / 16; ++t) qtile(std::false_type{}, buf, q0, t);
+    } else {
+#pragma unroll
+      for (int t = 0; t < QB2 / 16; ++t) qtile(std::true_type{}, buf, q0, t);
+    }
+    __syncthreads();  // all partials of the block written
+    if (stager) {
+      const int e = srow * HD + sc;
+      f32x4 sum = ld4(&dQr[0][e]);
+#pragma unroll
+      for (int u = 1; u < KW; ++u) sum += ld4(&dQr[u][e]);
+      if (q0 + srow < Tq) st4(part + (long)(q0 + srow) * (a.H * HD) + sc, sum);
+    }
+    if (qb + 1 < nqb) commit(buf ^ 1);
+  }
+
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int key = k0 + 16 * (KW * i + w) + kj;
+    if (key < Tk) {
+#pragma unroll
+      for (int dd = 0; dd < ND; ++dd) {
+        st4(P.dk + ((long)b * Tk + key) * a.ldk + h * HD + 16 * dd + 4 * grp, dk[i][dd]);
+        st4(P.dv + ((long)b * Tk + key) * a.ldv + h * HD + 16 * dd + 4 * grp, dv[i][dd] * P.dv_scale);
+      }
+    }
+  }
+}
+
+// dq = dq_scale * (sum over the key blocks' partials, in order); causal rows only have
+// partials from the key blocks at or before them
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const BwdArgs a) {
+  const sca_attn_bwd_problem& P = a.p[blockIdx.z];
+  const int d = a.H * 32, c4 = d / 4;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rows = (long)a.B * a.Tq;
+  if (e >= rows * c4) return;
+  const long row = e / c4;
+  const int c = (int)(e % c4) * 4;
+  const int q = (int)(row % a.Tq);
+  const int nkb = (a.Tk + KBLK - 1) / KBLK;
+  const int n = a.causal ? min(nkb, q / KBLK + 1) : nkb;
+  const long stride = rows * d;
+  f32x4 s = ld4(P.dq_part + row * d + c);
+  for (int kb = 1; kb < n; ++kb) s += ld4(P.dq_part + kb * stride + row * d + c);
+  st4(P.dq + row * a.ldq + c, s * P.dq_scale);
+}
+
 template <typename Args>
 int check_common(const Args& a, int hd, int nprob) {
   if (nprob < 1 || nprob > SCA_ATTN_MAX_PROBLEMS || a.B < 1 || a.H < 1 || a.Tq < 1 || a.Tk < 1) return 1;
@@ -795,6 +1066,14 @@ void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st) {
     else hipLaunchKernelGGL(attn_bwd_fused_kernel<false>, g, dim3(256), 0, st, a);
     return;
   }
+  if (HD == 32 && !AM && g_bwd_fused && a.p[0].dq_part) {
+    const dim3 g(a.B * a.H * gq.z, (a.Tk + KBLK - 1) / KBLK, 1);
+    if (a.causal) hipLaunchKernelGGL(attn_bwd_kblk_kernel<true>, g, dim3(64 * KW), 0, st, a);
+    else hipLaunchKernelGGL(attn_bwd_kblk_kernel<false>, g, dim3(64 * KW), 0, st, a);
+    const long n4 = (long)a.B * a.Tq * a.H * 32 / 4;
+    hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), 1, gq.z), dim3(256), 0, st, a);
+    return;
+  }
   if (a.causal) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, true>), gq, dim3(256), 0, st, a);
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, true>), gk, dim3(256), 0, st, a);
@@ -807,6 +1086,12 @@ void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st) {
 }  // namespace
 
 extern "C" void sca_set_error(const char* msg);
+
+// floats of dq_part per problem the fused hd-32 backward needs (0: that path does not apply)
+extern "C" long sca_attn_bwd_workspace(int B, int H, int Tq, int Tk, int hd) {
+  if (hd != 32 || B < 1 || H < 1 || Tq < 1 || Tk < 1) return 0;
+  return (long)((Tk + KBLK - 1) / KBLK) * B * Tq * H * hd;
+}
 
 extern "C" int sca_attn_bwd_fused(int enable) {
   g_bwd_fused = enable != 0;
@@ -870,6 +1155,10 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
       return SCA_ERR_ARG;
     }
     am = p.add_mask != nullptr;
+    if ((p.dq_part != nullptr) != (probs[0].dq_part != nullptr)) {
+      sca_set_error("sca_attn_bwd: all problems must agree on dq_part");
+      return SCA_ERR_ARG;
+    }
     a.p[i] = p;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -157,6 +157,7 @@ class GradBuckets:
         comm = self._comm_stream()
         for s in self._step["streams"][b].values():
             comm.wait_stream(s)  # the bucket's gradients are enqueued on these streams
+            ops.note_fork(comm, s, "RCCL stream")
         with torch.cuda.stream(comm):
             if self.average:
                 self._bucket(b).mul_(1.0 / self.world)
@@ -173,6 +174,7 @@ class GradBuckets:
             for s in st["producers"].values():
                 if s.cuda_stream != cur.cuda_stream:
                     cur.wait_stream(s)
+                    ops.note_join(cur, s)
         if self.plan is None:
             self._build_plan()
             self._fallback(list(range(len(self.params))))
@@ -190,6 +192,8 @@ class GradBuckets:
                 p.grad = self.flat[o:o + n].view(p.shape)
         for work in st["works"]:
             work.wait()  # GPU: the caller's stream waits for RCCL's stream; CPU: completes it
+        if st["works"] and cur is not None:
+            ops.note_join(cur, self._comm_stream())
         self._fallback([i for i, p in enumerate(self.params) if i not in self.slot and p.grad is not None])
 
     def _build_plan(self):

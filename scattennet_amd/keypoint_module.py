@@ -151,6 +151,7 @@ def sca_grouped(scas, xs, ys, attention_mask):
         main = torch.cuda.current_stream(se[0].device)
         _branch_stream(se[0].device, main)  # records the join target of the branch
         branch.wait_stream(main)
+        ops.note_fork(branch, main, "branch stream")
         for t in list(se) + [self_mask.key_valid]:
             t.record_stream(branch)
         with torch.cuda.stream(branch):
@@ -162,6 +163,7 @@ def sca_grouped(scas, xs, ys, attention_mask):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
         if i == 0 and branch is not None:
             main.wait_stream(branch)
+            ops.note_join(main, branch)
             for t in s:
                 t.record_stream(main)
         nxt = qkv_request([m.causal_attn_layers[i + 1] for m in scas]) if i + 1 < L else None

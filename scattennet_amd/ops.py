@@ -591,6 +591,82 @@ def branch_stream(device, origin=None):
     return st
 
 
+class ForkLedger:
+    """Host-side record of the stream forks and joins the hot path makes — weight-gradient side
+    streams (weight_grads), the branch stream (keypoint_module.sca_grouped), RCCL's stream
+    (dp.GradBuckets) — checked at the end of a graph capture: every stream forked during the
+    capture must afterwards be joined DIRECTLY into the capture's origin stream.  (DESIGN §7,
+    constraint (1): a forked stream joined into another forked stream that then joins the
+    origin crashed hipGraph instantiation; a fork never joined fails capture outright.)"""
+
+    def __init__(self, origin):
+        self.origin = origin.cuda_stream
+        self.seq = 0
+        self.last_fork = {}   # child stream -> seq of its last fork
+        self.last_join = {}   # child stream -> (seq, target) of its last join
+        self.names = {}
+
+    @staticmethod
+    def _id(st):
+        return st.cuda_stream if hasattr(st, "cuda_stream") else st
+
+    def fork(self, child, parent, name=""):
+        self.seq += 1
+        c = self._id(child)
+        if c != self.origin:
+            self.last_fork[c] = self.seq
+            self.names.setdefault(c, name)
+
+    def join(self, into, child):
+        self.seq += 1
+        self.last_join[self._id(child)] = (self.seq, self._id(into))
+
+    def problems(self):
+        out = []
+        for c, fs in self.last_fork.items():
+            j = self.last_join.get(c)
+            name = self.names.get(c) or hex(c)
+            if j is None or j[0] < fs:
+                out.append(f"stream {name} forked but not joined back")
+            elif j[1] != self.origin:
+                out.append(f"stream {name} joined into {hex(j[1])}, not into the capture origin")
+        return out
+
+    def check(self):
+        bad = self.problems()
+        if bad:
+            raise RuntimeError("fork/join check at capture end: " + "; ".join(bad))
+
+
+_LEDGER = None
+
+
+def fork_ledger_begin(origin=None):
+    """Start recording forks / joins (call inside the capture, on its origin stream)."""
+    global _LEDGER
+    _LEDGER = ForkLedger(origin if origin is not None else torch.cuda.current_stream())
+    return _LEDGER
+
+
+def fork_ledger_end():
+    """Stop recording; raise if a fork was not joined back into the origin."""
+    global _LEDGER
+    led, _LEDGER = _LEDGER, None
+    if led is not None:
+        led.check()
+    return led
+
+
+def note_fork(child, parent, name=""):
+    if _LEDGER is not None:
+        _LEDGER.fork(child, parent, name)
+
+
+def note_join(into, child):
+    if _LEDGER is not None:
+        _LEDGER.join(into, child)
+
+
 def _queue_join(main, side):
     key = (main.cuda_stream, side.cuda_stream)
     if _join_pending.get(key):
@@ -600,6 +676,7 @@ def _queue_join(main, side):
     def _join():
         _join_pending[key] = False
         main.wait_stream(side)
+        note_join(main, side)
 
     torch.autograd.Variable._execution_engine.queue_callback(_join)
 
@@ -641,6 +718,7 @@ def weight_grads(items, M=None, extra=None):
     else:
         side = _side_stream(dev)
     side.wait_stream(main)  # dY and X are ready on the main stream
+    note_fork(side, main, "weight-gradient side stream")
     for it in items:  # keep their memory from being reused by the main stream too early
         it[0].record_stream(side)
         it[1].record_stream(side)
@@ -747,13 +825,16 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
     dk = [torch.empty_like(t) for t in k]
     dv = [torch.empty_like(t) for t in v]
     delta = [q[0].new_empty(B * H * Tq) for _ in range(G)]
+    # the fused hd-32 backward (256-key blocks) writes per-key-block dQ partials
+    nws = L.lib().sca_attn_bwd_workspace(B, H, Tq, Tk, hd) if add_mask is None else 0
+    part = [q[0].new_empty(nws) for _ in range(G)] if nws > 0 else [None] * G
     for c in range(0, G, L.ATTN_MAX_PROBLEMS):
         gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
         arr = (L.AttnBwdProblem * len(gs))(*[
             L.AttnBwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
                              dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
                              ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
-                             delta[g].data_ptr(), dq_scale, dv_scale) for g in gs])
+                             delta[g].data_ptr(), dq_scale, dv_scale, ptr(part[g])) for g in gs])
         fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
         with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
             L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),

@@ -1,7 +1,7 @@
 """GPU parity of the fused attention kernels beyond the golden fixtures' shapes: every head
 size the kernels support (16 / 32 / 64), frame counts that are not multiples of the 64-row
-blocks, cross attention with Tq != Tk, all three mask kinds with ragged and fully padded
-clips — the drop-in modules against the CPU oracle (oracle/sca_oracle.py:attention), forward
+blocks, cross attention with Tq != Tk, hd 32 beyond one 256-key block (the fused key-block
+backward), all three mask kinds with ragged and fully padded clips — the drop-in modules against the CPU oracle (oracle/sca_oracle.py:attention), forward
 and all gradients within the north-star 1e-3.
 """
 import pytest
@@ -26,6 +26,11 @@ CASES = [  # kind, B, Tq, Tk, d, H
     ("causal", 3, 130, 130, 64, 4),   # partial last query block and key tile
     ("self", 3, 200, 200, 32, 2),
     ("cross", 2, 17, 250, 64, 4),
+    # hd 32 at any length: the fused backward over 256-key blocks + the dQ partial reduction
+    ("self", 2, 600, 600, 64, 2),     # three key blocks, the last partial
+    ("causal", 2, 520, 520, 64, 2),   # key blocks see only the queries after their first key
+    ("cross", 2, 300, 530, 64, 2),    # Tk > 256, Tq != Tk
+    ("causal", 1, 1024, 1024, 512, 16),  # BASELINE config 5's attention shape
 ]
 
 
@@ -37,8 +42,8 @@ def test_attention_shapes_vs_oracle(kind, B, Tq, Tk, d, H, fused):
     from scattennet_amd import _lib as L
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    if not fused and d // H != 16:
-        pytest.skip("the fused backward only exists for hd 16")
+    if not fused and d // H not in (16, 32):
+        pytest.skip("the fused backward only exists for hd 16 and 32")
     L.lib().sca_attn_bwd_fused(fused)
     try:
         _run_case(S, kind, B, Tq, Tk, d, H)

@@ -112,8 +112,11 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
         red.quiesce()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # RCCL watchdog thread
+            led = ops.fork_ledger_begin()
             outs = model(kp, mask)
             torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+            ops.fork_ledger_end()  # every fork (side streams, branch, RCCL) joined into the origin
+        assert led.last_fork and any("RCCL" in n for n in led.names.values())
         for p in params:  # poison the buckets: the replay must rewrite every planned gradient
             if p.grad is not None:
                 p.grad.fill_(float("nan"))

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--Tk", type=int, default=0, help="non-causal only: key length (default T)")
     ap.add_argument("--causal", default="0,1")
+    ap.add_argument("--split", action="store_true", help="hd 32: the split dq / dkdv kernels (no workspace)")
     a = ap.parse_args()
     lib = ctypes.CDLL(a.lib) if a.lib else L.lib()
     if a.lib:
@@ -71,12 +72,15 @@ def main():
     dk = [torch.empty_like(t) for t in k]
     dv = [torch.empty_like(t) for t in k]
     delta = [torch.empty(B * H * T, device=dev) for _ in range(G)]
+    nws = lib.sca_attn_bwd_workspace(B, H, T, Tk, hd) if not a.split else 0  # fused hd-32 key-block path
+    part = [torch.empty(nws, device=dev) if nws > 0 else None for _ in range(G)]
     P = lambda t: t.data_ptr()  # noqa: E731
     fwd = (L.AttnFwdProblem * G)(*[L.AttnFwdProblem(P(q[g]), P(k[g]), P(v[g]), P(o[g]), P(sm[g]), P(sl[g]),
                                                     P(kvalid), None) for g in range(G)])
     bwd = (L.AttnBwdProblem * G)(*[L.AttnBwdProblem(P(q[g]), P(k[g]), P(v[g]), P(o[g]), P(do[g]), P(sm[g]),
                                                     P(sl[g]), P(kvalid), None, P(dq[g]), P(dk[g]), P(dv[g]),
-                                                    P(delta[g]), 1.0, 1.0) for g in range(G)])
+                                                    P(delta[g]), 1.0, 1.0,
+                                                    P(part[g]) if part[g] is not None else None) for g in range(G)])
 
     for causal in [int(c) for c in a.causal.split(",")]:
         if causal and Tk != T:
