@@ -188,12 +188,17 @@ typedef struct {
   const float* gamma; /* [256] */
   float* dx;          /* [M, 256] gradient w.r.t. x */
   float* partial;     /* [2, nblk, 256] dgamma / dbeta partials */
-  /* optional chained GEMM (NULL = none): dout = dx Wo, Wo [256, 256] row-major (an
-   * nn.Linear weight [out, in]: dout is the gradient of the Linear's INPUT when dx is the
-   * gradient of its output) — the out-projection input gradient of the attention block that
-   * produced the LayerNorm input (attention.py:74 backwards), in the same launch           */
+  /* optional chained GEMM (NULL = none): dout = dx Wo, Wo [256, 256 * npass] row-major
+   * (an nn.Linear weight [out, in]: dout is the gradient of the Linear's INPUT when dx is the
+   * gradient of its output), in the same launch — the out-projection input gradient of the
+   * attention block that produced the LayerNorm input (attention.py:74 backwards, npass 1),
+   * or the FFN's dz = (dx W2) * gelu'(aux) (layers.py:104-107 backwards, npass 3, aux = the
+   * fc1 pre-activation)                                                                     */
   const float* wo;
-  float* dout;        /* [M, 256] */
+  float* dout;        /* [M, 256 * npass] */
+  const float* aux;   /* NULL, or [M, 256 * npass]: dout *= gelu'(aux) (exact-erf GELU) */
+  int npass;          /* 1..3 (0 reads as 1) */
+  int ldw;            /* row stride of wo, dout and aux (0 reads as 256 * npass) */
 } sca_gemm_lnb_problem;
 
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);

@@ -1292,14 +1292,17 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     const f32x4 ggx = gg * xh[i];
     s2[i] = (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
   }
-  // chained GEMM (dout = dx Wo): its first two B slices stream in under the LayerNorm math,
-  // into the V tile's region once every wave has read its rows of it
+  // chained GEMM (dout = dx Wo, npass 256-column blocks of Wo): its first two B slices
+  // stream in under the LayerNorm math, into the V tile's region once every wave has read
+  // its rows of it; the passes are one continuous slice sequence
   const bool chain = LN.wo != nullptr;
-  const float* pw = LN.wo + (long)(4 * wave) * LG_BN + 4 * lane;  // B pieces: k-rows 4*wave .. +3
-  auto dma2 = [&](int t, int stage) {
+  const int npass = chain ? max(LN.npass, 1) : 0;
+  const long ldw = LN.ldw ? LN.ldw : (long)LG_BN * npass;
+  const float* pw = LN.wo + (long)(4 * wave) * ldw + 4 * lane;  // B pieces: k-rows 4*wave .. +3
+  auto dma2 = [&](int u, int stage) {
+    const float* src = pw + (u >> 3) * LG_BN + (long)(32 * (u & 7)) * ldw;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      gl_dma(pw + (long)(32 * t + c) * LG_BN, smem + stage * LB_B2 + (4 * wave + c) * LB_BROW);
+    for (int c = 0; c < 4; ++c) gl_dma(src + c * ldw, smem + stage * LB_B2 + (4 * wave + c) * LB_BROW);
   };
   if (chain) {
     __syncthreads();
@@ -1340,18 +1343,22 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   LN.partial[(which * nblk + bx) * LG_BN + c] = sum;
   if (!chain) return;
 
-  // chained GEMM: dout[32 x 256] = dx_tile[32 x 256] Wo[256 x 256]; A from the LDS image
-  // (written above, published by the barrier), B through a 2-stage ring, one slice ahead
+  // chained GEMM: dout[32 x 256 npass] = dx_tile[32 x 256] Wo[256 x 256 npass]; A from the
+  // LDS image (written above, published by the barrier), B through a 2-stage ring, one
+  // slice ahead.  Passes before the last store straight from the accumulator (element form:
+  // the ring is busy with the next pass); the last one in row form after the loop.
+  const bool dgelu = LN.aux != nullptr;
   f32x16 acc2;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
-  constexpr int NS2 = LG_BN / GL_BK;  // 8 slices
-  for (int t = 0; t < NS2; ++t) {
+  const int nsl = 8 * npass;
+  for (int u = 0; u < nsl; ++u) {
     gl_wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t >= 1 && t + 1 < NS2) dma2(t + 1, (t + 1) & 1);  // into the stage slice t-1 left
-    const float* Bf = reinterpret_cast<const float*>(smem + (t & 1) * LB_B2);
+    if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
+    const int t = u & 7;
+    const float* Bf = reinterpret_cast<const float*>(smem + (u & 1) * LB_B2);
     f32x4 fa[4], fb[4];
 #pragma unroll
     for (int g2 = 0; g2 < 4; ++g2) {
@@ -1363,15 +1370,36 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     for (int g2 = 0; g2 < 4; ++g2)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc2 = mfma32(fa[g2][j], fb[g2][j], acc2);
+    if (t == 7 && u + 1 < nsl) {
+      // lane: column 32 wave + col of the pass, rows (r & 3) + 8 (r >> 2) + 4h
+      const long cn = (u >> 3) * LG_BN + 32 * wave + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= P.M) continue;
+        float o = acc2[r];
+        if (dgelu) o *= gelu_erf_grad(LN.aux[(long)m * ldw + cn]);
+        LN.dout[(long)m * ldw + cn] = o;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+    }
   }
   __syncthreads();  // ring free: wave-private transposition scratch (8 x 5 KB) for row stores
   f32x4 rows[4];
   acc_to_rows(acc2, reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD, lane, rows);
-  const int n2 = 32 * wave + 4 * (lane & 7);
+  const long n2 = (long)(npass - 1) * LG_BN + 32 * wave + 4 * (lane & 7);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + (lane >> 3) + 8 * i;
-    if (m < P.M) st4(LN.dout + (long)m * LG_BN + n2, rows[i]);
+    if (m >= P.M) continue;
+    f32x4 o = rows[i];
+    if (dgelu) {
+      const f32x4 ax = ld4(LN.aux + (long)m * ldw + n2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
+    }
+    st4(LN.dout + (long)m * ldw + n2, o);
   }
 }
 
@@ -1974,8 +2002,13 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
     uintptr_t al = reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
                    reinterpret_cast<uintptr_t>(L.x) | reinterpret_cast<uintptr_t>(L.gamma) |
                    reinterpret_cast<uintptr_t>(L.dx) | reinterpret_cast<uintptr_t>(L.wo) |
-                   reinterpret_cast<uintptr_t>(L.dout);
-    ok = ok && ((L.wo == nullptr) == (L.dout == nullptr));
+                   reinterpret_cast<uintptr_t>(L.dout) | reinterpret_cast<uintptr_t>(L.aux);
+    ok = ok && ((L.wo == nullptr) == (L.dout == nullptr)) && (L.wo || !L.aux);
+    if (L.wo) {
+      const int np = L.npass ? L.npass : 1;
+      const int ldw = L.ldw ? L.ldw : LG_BN * np;
+      ok = ok && L.npass >= 0 && L.npass <= 3 && (ldw & 3) == 0 && ldw >= LG_BN * np;
+    }
     for (int s = 0; ok && s < P.nseg; ++s) {
       const sca_gemm_seg& S = P.seg[s];
       ok = S.A && S.B && S.K >= GL_BK && S.K % GL_BK == 0 && (S.lda & 3) == 0 && S.lda >= S.K &&
@@ -1985,7 +2018,7 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
     if (!ok || (al & 15)) {
       sca_set_error("sca_gemm_lnb: needs N == 256, 1-3 segments with K a positive multiple of 32 and one alpha, "
                     "k-major B, no epilogue other than resid, 16-byte aligned operands with leading dimensions "
-                    "multiple of 4");
+                    "multiple of 4; chained: wo and dout both or neither, npass 0..3, ldw >= 256 npass");
       return SCA_ERR_ARG;
     }
     a.p[i] = P;

@@ -253,12 +253,15 @@ class LnSaved:
     its own input-gradient GEMM's epilogue (sca_gemm_lnb): the LN input v, its row mean /
     rstd and gamma.  `handoff` carries the result back to the producer's backward:
     (dL/dy as the consumer returned it, its version, dL/dv, dgamma/dbeta partials, nblk,
-    dout).  `wo`: the producer's out-projection weight when it is an attention block whose
-    next backward step is dO = dL/dv Wo (no dropout) — chained into the same launch, `dout`."""
-    __slots__ = ("v", "mean", "rstd", "gamma", "handoff", "wo")
+    dout).  `wo`: the producer's next backward GEMM on dL/dv, chained into the same launch
+    (`dout`) when no dropout sits between: an attention block's out-projection weight (dO =
+    dL/dv Wo) or an FFN's fc2 weight with `aux` = the fc1 pre-activation (dz = (dL/dv W2) *
+    gelu'(aux))."""
+    __slots__ = ("v", "mean", "rstd", "gamma", "handoff", "wo", "aux")
 
-    def __init__(self, v, mean, rstd, gamma, wo=None):
+    def __init__(self, v, mean, rstd, gamma, wo=None, aux=None):
         self.v, self.mean, self.rstd, self.gamma, self.handoff, self.wo = v, mean, rstd, gamma, None, wo
+        self.aux = aux
 
 
 def ln_saved_of(ts):
@@ -270,10 +273,20 @@ def ln_saved_of(ts):
 
 
 _CHAIN_DO = __import__("os").environ.get("SCA_CHAIN_DO", "1") != "0"
+# the FFN's dz chained into its consumer's sca_gemm_lnb launch: parity-green, but -1.7 % in
+# step at config 2 (three 256-column passes at one workgroup per CU lose to the stand-alone
+# NN GEMM that shares the CUs with the weight gradients; tools/ab_dz.sh) — off by default
+_CHAIN_DZ = __import__("os").environ.get("SCA_CHAIN_DZ", "0") != "0"
 
 
-def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None):
-    objs = [LnSaved(vs[g], means[g], rstds[g], gam[g], wo[g] if (wo is not None and _CHAIN_DO) else None)
+def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None, aux=None):
+    """wo[g]: [256, 256 npass] k-major (an nn.Linear weight [out = 256, in]); aux[g]: the
+    DGELU pre-activation [M, 256 npass] or None."""
+    ok = wo is not None and _CHAIN_DO and all(
+        w.dim() == 2 and w.shape[0] == 256 and w.shape[1] % 256 == 0 and w.shape[1] <= 768 and w.is_contiguous()
+        for w in wo)
+    objs = [LnSaved(vs[g], means[g], rstds[g], gam[g], wo[g] if ok else None,
+                    aux[g] if (ok and aux is not None) else None)
             for g in range(len(ys))]
     for y, o in zip(ys, objs):
         y._sca_ln = o
@@ -369,16 +382,19 @@ def gemm_lnb(probs, lnp):
     nblk = lib.sca_gemm_lnb_blocks(M)
     dv = [torch.empty_like(o.v) for o in lnp]
     part = [o.v.new_empty(2 * nblk * o.v.shape[-1]) for o in lnp]
-    chain = all(o.wo is not None for o in lnp)  # the producers' dO = dv Wo in the same launch
-    dout = [torch.empty_like(o.v) for o in lnp] if chain else [None] * len(lnp)
+    # the producers' next GEMM on dv (dO = dv Wo, or dz = (dv W2) gelu'(z)) in the same launch
+    chain = all(o.wo is not None for o in lnp) and len({(o.wo.shape[1], o.aux is None) for o in lnp}) == 1
+    n2 = lnp[0].wo.shape[1] if chain else 0
+    dout = [o.v.new_empty(*o.v.shape[:-1], n2) for o in lnp] if chain else [None] * len(lnp)
     arr = (L.GemmProblem * len(probs))(*probs)
     larr = (L.GemmLnbProblem * len(lnp))(*[L.GemmLnbProblem(o.v.data_ptr(), o.mean.data_ptr(), o.rstd.data_ptr(),
                                                            o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr(),
-                                                           ptr(o.wo) if chain else None, ptr(dout[g]))
+                                                           ptr(o.wo) if chain else None, ptr(dout[g]),
+                                                           ptr(o.aux) if chain else None, n2 // 256, n2)
                                             for g, o in enumerate(lnp)])
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
-        flops += sum(2.0 * p.M * 256 * 256 for p in probs)
+        flops += sum(2.0 * p.M * 256 * n2 for p in probs)
     with _timed("gemm_lnb_kernel", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
@@ -1099,7 +1115,10 @@ class FeedForwardResidual(Function):
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
         ctx.b1, ctx.b2, ctx.bet = tuple(b1), tuple(b2), (tuple(bet) if ln else ())  # parameters (leaves)
-        ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam) if ln else None
+        # dz = (dL/dv W2) * gelu'(z) chained into the consumer's launch (no dropout in between)
+        dz_chain = drop_p == 0 and _CHAIN_DZ
+        ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, W2 if dz_chain else None,
+                                       zs if dz_chain else None) if ln else None
         ctx.lnprev = lnprev if (lnprev is not None and d == 256 and has_r and F_ % 32 == 0) else None
         ctx.save_for_backward(*x, *W1, *W2, *zs, *acts, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
@@ -1110,10 +1129,10 @@ class FeedForwardResidual(Function):
         sv = ctx.saved_tensors
         x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
         dgam = dbet = ()
-        ln_finish = None
+        ln_finish = dzc = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
             vs, gam, means, rstds = (sv[(5 + i) * G:(6 + i) * G] for i in range(4))
-            dys, dgam, dbet, ln_finish, _ = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
+            dys, dgam, dbet, ln_finish, dzc = _ln_bwd_or_handoff(dys, vs, gam, means, rstds, ctx.lnsaved, ctx.bet)
             dgam, dbet = tuple(dgam), tuple(dbet)
         else:
             dys = _contig(_zeros_for_none(dys, x))
@@ -1125,10 +1144,13 @@ class FeedForwardResidual(Function):
         if p > 0:
             dyo = [torch.empty_like(t) for t in dys]
             dropout_apply([(dys[g], dyo[g], ctx.s2[g]) for g in range(G)], p)
-        dz = [x[0].new_empty(M, F_) for _ in range(G)]
-        # dz = mask1 * (dy' W2) * gelu'(z)
-        gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
-                               aux=zs[g], ldx=F_, drop=(ctx.s1[g], p) if p > 0 else None) for g in range(G)])
+        # dz = mask1 * (dy' W2) * gelu'(z) — or already computed by the consumer's launch
+        if dzc is not None and p == 0:
+            dz = [t.reshape(M, F_) for t in dzc]
+        else:
+            dz = [x[0].new_empty(M, F_) for _ in range(G)]
+            gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
+                                   aux=zs[g], ldx=F_, drop=(ctx.s1[g], p) if p > 0 else None) for g in range(G)])
         # dx = dz W1 + dy   (residual); with `lnprev` the input's LayerNorm backward rides in
         # the same launch (sca_gemm_lnb)
         dx = [torch.empty_like(x[g]) for g in range(G)]

@@ -26,9 +26,12 @@ def _need_gpu():
         pytest.skip("needs a GPU")
 
 
-@pytest.mark.parametrize("chain", [False, True])
+@pytest.mark.parametrize("chain", ["none", "wo", "dgelu3", "ld2"])
 @pytest.mark.parametrize("M,Ks", [(2048, (768,)), (2048, (256, 256, 256)), (1000, (256,)), (33, (32, 64))])
 def test_gemm_lnb_c_abi_vs_float64(M, Ks, chain):
+    """chain: none; "wo": dout = dx Wo (one pass, the attention out-projection input
+    gradient); "dgelu3": dout = (dx W2) * gelu'(aux) over three 256-column passes (the FFN's
+    dz); "ld2": two passes with row stride 640 (ldw > 256 npass)."""
     _need_gpu()
     from scattennet_amd import _lib as L, ops
     dev = torch.device("cuda:0")
@@ -51,9 +54,15 @@ def test_gemm_lnb_c_abi_vs_float64(M, Ks, chain):
     nblk = L.lib().sca_gemm_lnb_blocks(M)
     part = torch.empty(2 * nblk * N, device=dev)
     prob = ops._prob(segs, C, M, N, N, resid=resid, ldr=N)
-    wo, dout = torch.randn(N, N, device=dev) / N ** 0.5, torch.full((M, N), float("nan"), device=dev)
+    npass, ldw = {"none": (0, 0), "wo": (1, 256), "dgelu3": (3, 768), "ld2": (2, 640)}[chain]
+    wo = torch.randn(N, max(ldw, N), device=dev) / N ** 0.5
+    dout = torch.full((M, max(ldw, N)), float("nan"), device=dev)
+    aux = torch.randn(M, max(ldw, N), device=dev) if chain == "dgelu3" else None
+    on = chain != "none"
     lnp = L.GemmLnbProblem(x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gam.data_ptr(), dx.data_ptr(),
-                           part.data_ptr(), wo.data_ptr() if chain else None, dout.data_ptr() if chain else None)
+                           part.data_ptr(), wo.data_ptr() if on else None, dout.data_ptr() if on else None,
+                           aux.data_ptr() if aux is not None else None, npass if chain != "wo" else 0,
+                           ldw if chain == "ld2" else 0)
     arr, larr = (L.GemmProblem * 1)(prob), (L.GemmLnbProblem * 1)(lnp)
     L.check(L.lib().sca_gemm_lnb(1, arr, larr, L.stream_handle()), "sca_gemm_lnb")
     torch.cuda.synchronize()
@@ -68,8 +77,16 @@ def test_gemm_lnb_c_abi_vs_float64(M, Ks, chain):
     pb = part[nblk * N:].view(nblk, N).sum(0).cpu()
     assert rel_err(pg, g64.grad) < 1e-4
     assert rel_err(pb, b64.grad) < 1e-4
-    if chain:  # the chained out-projection input gradient: dout = dx Wo
-        assert rel_err(dout.cpu(), x64.grad @ wo.double().cpu()) < 1e-4
+    if on:  # the chained GEMM: dout = dx Wo (* gelu'(aux))
+        n = 256 * npass
+        want = x64.grad @ wo.double().cpu()[:, :n]
+        if aux is not None:
+            z = aux.double().cpu()[:, :n].requires_grad_(True)
+            torch.nn.functional.gelu(z).backward(torch.ones_like(z))
+            want = want * z.grad
+        assert rel_err(dout.cpu()[:, :n], want) < 1e-4
+        if chain == "ld2":
+            assert torch.isnan(dout[:, n:]).all()  # columns past the passes untouched
 
 
 def test_gemm_lnb_rejects_bad_shapes():
@@ -85,11 +102,15 @@ def test_gemm_lnb_rejects_bad_shapes():
                                      L.stream_handle()), "sca_gemm_lnb")
 
 
+@pytest.mark.parametrize("dz", [True, False])
 @pytest.mark.parametrize("second_consumer", [False, True])
-def test_chained_blocks_hand_off_layer_norm_backward(second_consumer):
+def test_chained_blocks_hand_off_layer_norm_backward(second_consumer, dz, monkeypatch):
+    """... and with `dz` block 0's FFN dz = (dL/dv W2) * gelu'(z) rides in block 1's
+    gemm_lnb launch too (one NN launch fewer) unless a second consumer blocks the hand-off."""
     _need_gpu()
     import scattennet_amd as S
-    from scattennet_amd import ops, workloads as W
+    from scattennet_amd import _lib as L, ops, workloads as W
+    monkeypatch.setattr(ops, "_CHAIN_DZ", dz)
     dev = torch.device("cuda:0")
     torch.manual_seed(5)
     B, T, d, H = 3, 96, 256, 16
@@ -121,6 +142,10 @@ def test_chained_blocks_hand_off_layer_norm_backward(second_consumer):
     # hand-offs: block 1's FFN -> its attention LN; block 1's attention -> block 0's last LN;
     # block 0's FFN -> its attention LN (block 0's attention input x has no fused producer)
     assert prof.stats().get("gemm_lnb_kernel", {}).get("launches", 0) == 3
+    # NN launches: block 0's attention dX (no fused producer), block 1's FFN dz (its output has
+    # no fused consumer) and block 0's FFN dz unless block 1's launch chained it
+    nn = prof.stats().get(ops._GEMM_NAMES[L.GEMM_NN], {}).get("launches", 0)
+    assert nn == (2 if dz and not second_consumer else 3), nn
 
     ps = [{k: v.detach().cpu().clone().requires_grad_(True) for k, v in blk.state_dict().items()} for blk in blocks]
     xr = x.clone().requires_grad_(True)
