@@ -87,9 +87,10 @@ class CoordinatesMerge(nn.Module):
         return coordinates_merge_grouped([self], [y_embed], [x_embed], cross_attn_mask)[0]
 
 
-def coordinates_merge_grouped(blocks, ys, xs, mask, nxt=None):
+def coordinates_merge_grouped(blocks, ys, xs, mask, nxt=None, kvacc=None):
     h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True, drop_p=drop_p(blocks),
-                          ln=[b.attn_layer_norm for b in blocks], nxt=fc1_request([b.mlp for b in blocks]))
+                          ln=[b.attn_layer_norm for b in blocks], nxt=fc1_request([b.mlp for b in blocks]),
+                          kvacc=kvacc)
     return ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks], nxt=nxt)
 
 
@@ -159,6 +160,9 @@ def sca_grouped(scas, xs, ys, attention_mask):
     else:
         s = _self_stack(scas, s, self_mask, L)
     c = ce
+    # the merge layers all read the final x-stream map s; their backward runs L-1 .. 0, so
+    # its gradient accumulates in their GEMM epilogues instead of L-1 autograd adds
+    kvacc = ops.KvGradAccumulator() if (ops._KV_ACC and L > 1) else None
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
         if i == 0 and branch is not None:
@@ -167,7 +171,8 @@ def sca_grouped(scas, xs, ys, attention_mask):
             for t in s:
                 t.record_stream(main)
         nxt = qkv_request([m.causal_attn_layers[i + 1] for m in scas]) if i + 1 < L else None
-        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask, nxt=nxt)
+        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask, nxt=nxt,
+                                      kvacc=(kvacc, i) if kvacc is not None else None)
     return c, s
 
 

@@ -858,6 +858,25 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
     return dq, dk, dv
 
 
+class KvGradAccumulator:
+    """One key/value input shared by a chain of cross-attention blocks whose backward passes
+    run strictly in reverse chain order (keypoint_module.sca_grouped: every merge layer reads
+    the final x-stream map, and merge i+1 consumes merge i's output).  Instead of returning
+    one gradient each for autograd to add up (3 elementwise adds per stream), the blocks'
+    key/value input-gradient GEMMs accumulate into one buffer (the first to run writes it, the
+    others add to it in their GEMM epilogue, SCA_EPI_ACCUM); the LAST block of the chain
+    (index 0, the last backward to run) returns the buffer and the others return None."""
+
+    def __init__(self):
+        self.buf = None
+
+
+# parity-green, but -1.6 % in step at config 2 (tools/ab_kvacc.sh: 1558 vs 1584 clips/s over
+# three alternations) — the autograd adds it removes run on the branch stream beside the
+# main stream's work, off the critical path; off by default (SCA_KV_ACC=1)
+_KV_ACC = __import__("os").environ.get("SCA_KV_ACC", "0") != "0"
+
+
 class AttentionBlock(Function):
     """One attention operator end to end, G streams per launch:
 
@@ -871,7 +890,7 @@ class AttentionBlock(Function):
     into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, *ts):
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, kvacc, *ts):
         cross = kind == "cross"
         ln = ln_eps is not None  # post-LN LayerNorm fused into the out-projection (sca_gemm_ln)
         if ln:
@@ -929,6 +948,7 @@ class AttentionBlock(Function):
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
+        ctx.kvacc = kvacc if cross else None  # (KvGradAccumulator, index in the chain)
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
         ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, Wo if drop_p == 0 else None) if ln else None
@@ -981,15 +1001,20 @@ class AttentionBlock(Function):
         # input gradients (residual gradient fused as the epilogue's resid term); with `lnprev`
         # the query input's LayerNorm backward rides in the same launch (sca_gemm_lnb)
         dxq, dxkv, probs, kvprobs = [], [], [], []
+        acc = ctx.kvacc[0] if ctx.kvacc is not None else None
+        accum = acc is not None and acc.buf is not None  # an earlier (later-layer) block wrote it
+        if acc is not None and acc.buf is None:
+            acc.buf = [torch.empty_like(t) for t in xkv]
         for g in range(G):
             Wq, _, Wk, _, Wv, _ = W[6 * g:6 * g + 6]
             dqf, dkf, dvf = _flat(dq[g]), _flat(dk[g]), _flat(dv[g])
             r = _flat(dys[g]) if ctx.has_resid else None
             gx = torch.empty_like(xq[g])
             if cross:
-                gkv = torch.empty_like(xkv[g])
+                gkv = acc.buf[g] if acc is not None else torch.empty_like(xkv[g])
                 probs.append(_prob([_seg(dqf, Wq, d, d, d)], gx, B * T, d, d, resid=r, ldr=d))
-                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
+                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d,
+                                     epi=L.EPI_ACCUM if accum else 0))
                 dxkv.append(gkv)
             else:
                 probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
@@ -1016,7 +1041,12 @@ class AttentionBlock(Function):
                 dW += list(wg[4 * g + j])
             dWo.append(wg[4 * g + 3][0])
             dbo.append(wg[4 * g + 3][1])
-        return (None,) * 11 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
+        if acc is not None:  # the chain's last backward hands the accumulated gradient over
+            if ctx.kvacc[1] == 0:
+                acc.buf = None
+            else:
+                dxkv = [None] * G
+        return (None,) * 12 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
             tuple(dbo) + dgam + dbet
 
 

@@ -285,3 +285,34 @@ def test_sca_stack_chained_projections_vs_oracle(chain, monkeypatch):
     for k, v in p.items():
         if v.grad is not None:
             assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))
+
+
+def test_sca_stack_kv_gradient_accumulated_in_epilogue(monkeypatch):
+    """SCA_KV_ACC: the merge layers' key/value input gradients (all of them w.r.t. the final
+    x-stream map) accumulated in the GEMM epilogue (ops.KvGradAccumulator) give the same
+    gradients as autograd's sum — three-layer stack, also when the x-stream map is itself
+    part of the loss (a second consumer of the accumulated gradient)."""
+    _need_gpu()
+    import scattennet_amd as S
+    from scattennet_amd import ops
+    from scattennet_amd.workloads import model_cfg
+    dev = torch.device("cuda:0")
+    torch.manual_seed(5)
+    B, T, d, H = 2, 64, 256, 16
+    cfg = model_cfg(d, H, 3, maxpos=T)
+    m = S.SeparativeCoordinateAttention(cfg).to(dev)
+    x, y = torch.randn(B, T, d, device=dev), torch.randn(B, T, d, device=dev)
+    mask = torch.ones(B, T, dtype=torch.long, device=dev)
+    mask[1, 40:] = 0
+    g1, g2 = torch.randn(B, T, d, device=dev), torch.randn(B, T, d, device=dev)
+    grads = []
+    for acc in (False, True):
+        monkeypatch.setattr(ops, "_KV_ACC", acc)
+        m.zero_grad(set_to_none=True)
+        xg, yg = x.clone().requires_grad_(True), y.clone().requires_grad_(True)
+        out = m(xg, yg, mask, return_attn_map=True)
+        ((out["outputs"] * g1).sum() + (out["self_attn_map"] * g2).sum()).backward()
+        torch.cuda.synchronize()
+        grads.append([xg.grad.clone(), yg.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        assert rel_err(b, a) < 1e-5
