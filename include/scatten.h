@@ -229,6 +229,12 @@ typedef struct {
   float* stat_ll; /* [B*H*Tq] */
   const float* key_valid; /* [B, Tk] 1.0/0.0, or NULL */
   const float* add_mask;  /* [B, Tq, Tk] additive, or NULL */
+  /* attention-probability dropout (attention.py:67-69, 119-121, 173-175), drop_p = 0: none.
+   * O = (P * keep / (1 - drop_p)) V with keep = the sca_dropout mask of drop_seed over the
+   * (B, H, Tq, Tk) probabilities, element e = ((b H + h) Tq + i) Tk + j (mod 2^32); the
+   * softmax statistics are those of P.  The backward must get the same seed and p.        */
+  unsigned long long drop_seed;
+  float drop_p;
 } sca_attn_fwd_problem;
 
 typedef struct {
@@ -250,6 +256,8 @@ typedef struct {
   float* dq_part; /* workspace of sca_attn_bwd_workspace() floats, or NULL: with it (hd 32, no
                      add_mask) the backward is one fused launch over 256-key blocks + a
                      fixed-order dQ reduction; without it the split dq / dkdv kernels */
+  unsigned long long drop_seed; /* the forward's attention-probability dropout */
+  float drop_p;
 } sca_attn_bwd_problem;
 
 #define SCA_ATTN_MAX_PROBLEMS 8

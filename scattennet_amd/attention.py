@@ -102,9 +102,14 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
     accumulated over a chain of blocks sharing it (index 0 = the chain's first block)."""
     G = len(attns)
     a0 = attns[0]
-    for a in attns:
-        if a.training and a.dropout > 0:
-            raise NotImplementedError("attention dropout > 0 in training mode is not implemented")
+    # attention-probability dropout (attention.py:67-69 / 119-121 / 173-175): F.dropout(p,
+    # training=self.training); the grouped modules must share p and mode
+    ps = {float(a.dropout) if a.training else 0.0 for a in attns}
+    if len(ps) != 1:
+        raise ValueError("grouped attention modules must share dropout and training mode")
+    attn_p = ps.pop()
+    if not 0.0 <= attn_p < 1.0:
+        raise ValueError(f"dropout probability has to be in [0, 1), but got {attn_p}")
     causal = kind == "causal"
     hq = hidden[0]
     if hq.dim() != 3:
@@ -122,7 +127,7 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
         ts += [n.weight for n in ln] + [n.bias for n in ln]
     out = list(ops.AttentionBlock.apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
                                         bool(resid), float(drop_p), float(ln[0].eps) if fuse else None,
-                                        nxt if fuse else None, kvacc if kind == "cross" else None, *ts))
+                                        nxt if fuse else None, kvacc if kind == "cross" else None, attn_p, *ts))
     if ln is not None and not fuse:
         from .layers import layernorm_grouped
         out = layernorm_grouped(ln, out)

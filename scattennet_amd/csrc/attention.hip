@@ -48,12 +48,20 @@ constexpr float L2E = SCA_LOG2E;
 struct FwdArgs {
   sca_attn_fwd_problem p[SCA_ATTN_MAX_PROBLEMS];
   int B, H, Tq, Tk, ldq, ldk, ldv, ldo, causal, plus_one;
+  const unsigned long long* drop_off;  // dropout step counter (sca_dropout_offset) or NULL
 };
 
 struct BwdArgs {
   sca_attn_bwd_problem p[SCA_ATTN_MAX_PROBLEMS];
   int B, H, Tq, Tk, ldq, ldk, ldv, ldo, causal, plus_one;
+  const unsigned long long* drop_off;
 };
+
+// attention-probability dropout (DROP kernels): the sca_dropout mask of the problem's seed
+// over the (B, H, Tq, Tk) probabilities, element ((b H + h) Tq + i) Tk + j (mod 2^32)
+__device__ __forceinline__ uint32_t drop_row(int b, int H, int h, int Tq, int Tk, int i) {
+  return ((uint32_t)(b * H + h) * (uint32_t)Tq + (uint32_t)i) * (uint32_t)Tk;
+}
 
 using DiagStep = std::true_type;
 using FullStep = std::false_type;
@@ -158,7 +166,7 @@ __device__ __forceinline__ TileId xcd_tile() {
 }
 
 // ------------------------------------------------------------------------------ forward
-template <int HD, bool ADDMASK, bool CAUSAL>
+template <int HD, bool ADDMASK, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
   constexpr int NS = HD / 4;   // MFMA k-steps over the head dim
   constexpr int ND = HD / 16;  // 16-wide output d-blocks
@@ -180,6 +188,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
   const int qi = lane & 15, grp = lane >> 4;
   const int qrow = q0 + 16 * w + qi;
   const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
+  DropMask dm;
+  if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
+  const uint32_t erow = drop_row(b, a.H, h, a.Tq, a.Tk, qrow);
 
   // Q fragment: lane holds Q[qrow][NS*grp + s], s < NS (B operand of S^T = K Q^T)
   float qreg[NS];
@@ -269,8 +280,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = fast_exp2(sv[t][r] - m_new);
-        sv[t][r] = p;
-        psum += p;
+        psum += p;  // the row sum (softmax statistics) of the undropped probabilities
+        sv[t][r] = DROP ? dm.apply(erow + (uint32_t)(kb + 16 * t + 4 * grp + r), p) : p;
       }
     l_run = l_run * alpha + psum;
 #pragma unroll
@@ -310,7 +321,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dQ
-template <int HD, bool ADDMASK, bool CAUSAL>
+template <int HD, bool ADDMASK, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   constexpr int NS = HD / 4;
   constexpr int ND = HD / 16;
@@ -361,6 +372,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   const float mrow = P.stat_m[si], llrow = P.stat_ll[si];
   if (qok && grp == 0) P.delta[si] = delta;
   const float* amrow = ADDMASK ? P.add_mask + ((long)b * a.Tq + qc) * a.Tk : nullptr;
+  DropMask dm;
+  if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
+  const uint32_t erow = drop_row(b, a.H, h, a.Tq, a.Tk, qrow);
 
   f32x4 dq[ND];
 #pragma unroll
@@ -417,7 +431,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
         else t2 = fmaf(s_acc[r], L2E, ad[r]);
         if (DIAG && t == w && 4 * grp + r > qi) t2 = -INFINITY;
         const float p = fast_exp2((t2 - mrow) - llrow);
-        ds[r] = p * (dp_acc[r] - delta);
+        // dropout: dP = dP' * keep / (1 - p); delta = rowsum(dO * O) is unchanged
+        const float dpk = DROP ? dm.apply(erow + (uint32_t)(kb + kl + r), dp_acc[r]) : dp_acc[r];
+        ds[r] = p * (dpk - delta);
       }
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
@@ -441,7 +457,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dK, dV
-template <int HD, bool ADDMASK, bool CAUSAL>
+template <int HD, bool ADDMASK, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
   constexpr int NS = HD / 4;
   constexpr int ND = HD / 16;
@@ -482,6 +498,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
     }
   }
   const float kadd = key_add(kv_load(P.key_valid, b, krow, a.Tk), ADDMASK, krow, a.Tk, plus2);
+  DropMask dm;
+  if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
+  const uint32_t ekey = drop_row(b, a.H, h, a.Tq, a.Tk, 0) + (uint32_t)krow;
 
   f32x4 dk[ND], dv[ND];
 #pragma unroll
@@ -555,7 +574,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
         }
         if (DIAG && t == w && kj > 4 * grp + r) t2 = -INFINITY;
         p[r] = fast_exp2((t2 - sm[r]) - sl[r]);
-        ds[r] = p[r] * (dp_acc[r] - sd[r]);
+        if (DROP) {  // dV uses the dropped probabilities; dP = dP' * keep / (1 - p)
+          const uint32_t e = ekey + (uint32_t)(qb + ql + r) * (uint32_t)a.Tk;
+          ds[r] = p[r] * (dm.apply(e, dp_acc[r]) - sd[r]);
+          p[r] = dm.apply(e, p[r]);
+        } else {
+          ds[r] = p[r] * (dp_acc[r] - sd[r]);
+        }
       }
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
@@ -606,7 +631,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
 constexpr int FB_TMAX = 256;
 constexpr int FB_TS = 20;  // row stride of the 16x16 dS transposition tile (16 + 4 pad)
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a) {
   constexpr int HD = 16, NS = 4;
   __shared__ __attribute__((aligned(16))) float Qs[2][QB * HD];
@@ -624,6 +649,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
   const int kj = lane & 15, grp = lane >> 4;
   const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
   const int Tq = a.Tq, Tk = a.Tk;
+  DropMask dm;
+  if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
+  const uint32_t ebase = drop_row(b, a.H, h, Tq, Tk, 0);
 
   // own key tiles: K, V rows (B operands of S = Q K^T, dP = dO V^T) and K^T fragments
   // (A operand of dQ^T = K^T dS^T: lane (d = kj, grp) holds K[16g + 4grp + r][d])
@@ -725,7 +753,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
           float t2 = fmaf(s_acc[r], L2E, kadd[i]);
           if (CAUSAL && g == 4 * qb + t && kj > 4 * grp + r) t2 = -INFINITY;
           p[r] = fast_exp2((t2 - sm[r]) - sl[r]);
-          ds[r] = p[r] * (dp_acc[r] - sd[r]);
+          if (DROP) {  // dV uses the dropped probabilities; dP = dP' * keep / (1 - p)
+            const uint32_t e = ebase + (uint32_t)(qb * QB + ql + r) * (uint32_t)Tk + (uint32_t)(16 * g + kj);
+            ds[r] = p[r] * (dm.apply(e, dp_acc[r]) - sd[r]);
+            p[r] = dm.apply(e, p[r]);
+          } else {
+            ds[r] = p[r] * (dp_acc[r] - sd[r]);
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -788,7 +822,7 @@ __device__ __forceinline__ f32x4 col_frag32(const float* img, int d, int slot) {
   return ld4(img + d * QB2 + 4 * (slot ^ ((d >> 1) & 7)));
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs a) {
   constexpr int HD = 32, NS = 8, ND = 2, TPW = KBLK / 16 / KW;
   __shared__ __attribute__((aligned(16))) float Qs[2][QB2 * HD];
@@ -813,6 +847,9 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
   const float plus2 = (CAUSAL && a.plus_one) ? L2E : 0.0f;
   const int Tq = a.Tq, Tk = a.Tk;
   const int k0 = tid.x * KBLK;
+  DropMask dm;
+  if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
+  const uint32_t ebase = drop_row(b, a.H, h, Tq, Tk, 0);
 
   // own key tiles g = KW i + w: K, V rows (lane (kj, grp): d = 8 grp .. 8 grp + 7) and the K^T
   // fragments of both 16-wide d blocks (lane (d = 16 dd + kj, grp): K[16g + 4grp + r][d])
@@ -947,7 +984,13 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
         float t2 = fmaf(s_acc[r], L2E, kadd[i]);
         if (GEN && CAUSAL && g == qt && kj > 4 * grp + r) t2 = -INFINITY;
         p[r] = fast_exp2((t2 - sm[r]) - sl[r]);
-        ds[r] = p[r] * (dp_acc[r] - sd[r]);
+        if (DROP) {  // dV uses the dropped probabilities; dP = dP' * keep / (1 - p)
+          const uint32_t e = ebase + (uint32_t)(q0 + ql + r) * (uint32_t)Tk + (uint32_t)(16 * g + kj);
+          ds[r] = p[r] * (dm.apply(e, dp_acc[r]) - sd[r]);
+          p[r] = dm.apply(e, p[r]);
+        } else {
+          ds[r] = p[r] * (dp_acc[r] - sd[r]);
+        }
       }
 #pragma unroll
       for (int dd = 0; dd < ND; ++dd)
@@ -1050,37 +1093,49 @@ int check_common(const Args& a, int hd, int nprob) {
   return 0;
 }
 
-template <int HD, bool AM>
+template <int HD, bool AM, bool DR>
 void launch_fwd(const FwdArgs& a, dim3 grid, hipStream_t st) {
-  if (a.causal) hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, false>), grid, dim3(256), 0, st, a);
+  if (a.causal) hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, true, DR>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<HD, AM, false, DR>), grid, dim3(256), 0, st, a);
+}
+
+template <int HD, bool AM>
+void launch_fwd(const FwdArgs& a, dim3 grid, hipStream_t st, bool drop) {
+  if (drop) launch_fwd<HD, AM, true>(a, grid, st);
+  else launch_fwd<HD, AM, false>(a, grid, st);
 }
 
 bool g_bwd_fused = true;
 
-template <int HD, bool AM>
+template <int HD, bool AM, bool DR>
 void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st) {
   if (HD == 16 && !AM && g_bwd_fused && a.Tq <= FB_TMAX && a.Tk <= FB_TMAX) {
     const dim3 g(1, a.B * a.H, gq.z);
-    if (a.causal) hipLaunchKernelGGL(attn_bwd_fused_kernel<true>, g, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(attn_bwd_fused_kernel<false>, g, dim3(256), 0, st, a);
+    if (a.causal) hipLaunchKernelGGL((attn_bwd_fused_kernel<true, DR>), g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_fused_kernel<false, DR>), g, dim3(256), 0, st, a);
     return;
   }
   if (HD == 32 && !AM && g_bwd_fused && a.p[0].dq_part) {
     const dim3 g(a.B * a.H * gq.z, (a.Tk + KBLK - 1) / KBLK, 1);
-    if (a.causal) hipLaunchKernelGGL(attn_bwd_kblk_kernel<true>, g, dim3(64 * KW), 0, st, a);
-    else hipLaunchKernelGGL(attn_bwd_kblk_kernel<false>, g, dim3(64 * KW), 0, st, a);
+    if (a.causal) hipLaunchKernelGGL((attn_bwd_kblk_kernel<true, DR>), g, dim3(64 * KW), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_kblk_kernel<false, DR>), g, dim3(64 * KW), 0, st, a);
     const long n4 = (long)a.B * a.Tq * a.H * 32 / 4;
     hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), 1, gq.z), dim3(256), 0, st, a);
     return;
   }
   if (a.causal) {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, true>), gq, dim3(256), 0, st, a);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, true>), gk, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, true, DR>), gq, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, true, DR>), gk, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, false>), gq, dim3(256), 0, st, a);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, false>), gk, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, AM, false, DR>), gq, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HD, AM, false, DR>), gk, dim3(256), 0, st, a);
   }
+}
+
+template <int HD, bool AM>
+void launch_bwd(const BwdArgs& a, dim3 gq, dim3 gk, hipStream_t st, bool drop) {
+  if (drop) launch_bwd<HD, AM, true>(a, gq, gk, st);
+  else launch_bwd<HD, AM, false>(a, gq, gk, st);
 }
 
 }  // namespace
@@ -1103,13 +1158,14 @@ extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B,
   FwdArgs a;
   a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
   a.causal = causal; a.plus_one = plus_one;
+  a.drop_off = sca_drop_offset_ptr();
   const int err = check_common(a, hd, nprob);
   if (err) {
     sca_set_error(err == 2 ? "sca_attn_fwd: head_dim must be 16, 32 or 64"
                            : "sca_attn_fwd: bad shape / leading dimension / causal with Tq != Tk");
     return SCA_ERR_ARG;
   }
-  bool am = false;
+  bool am = false, drop = false;
   for (int i = 0; i < nprob; ++i) {
     a.p[i] = probs[i];
     if (!probs[i].q || !probs[i].k || !probs[i].v || !probs[i].o || !probs[i].stat_m || !probs[i].stat_ll) {
@@ -1121,13 +1177,18 @@ extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B,
       return SCA_ERR_ARG;
     }
     am = probs[i].add_mask != nullptr;
+    if (!(probs[i].drop_p >= 0.f && probs[i].drop_p < 1.f)) {
+      sca_set_error("sca_attn_fwd: drop_p must be in [0, 1)");
+      return SCA_ERR_ARG;
+    }
+    drop = drop || probs[i].drop_p > 0.f;
   }
   const int nqb = (Tq + QB - 1) / QB;  // causal: two paired query blocks per workgroup
   dim3 grid(causal ? (nqb + 1) / 2 : nqb, B * H, nprob);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hd == 16) am ? launch_fwd<16, true>(a, grid, st) : launch_fwd<16, false>(a, grid, st);
-  else if (hd == 32) am ? launch_fwd<32, true>(a, grid, st) : launch_fwd<32, false>(a, grid, st);
-  else am ? launch_fwd<64, true>(a, grid, st) : launch_fwd<64, false>(a, grid, st);
+  if (hd == 16) am ? launch_fwd<16, true>(a, grid, st, drop) : launch_fwd<16, false>(a, grid, st, drop);
+  else if (hd == 32) am ? launch_fwd<32, true>(a, grid, st, drop) : launch_fwd<32, false>(a, grid, st, drop);
+  else am ? launch_fwd<64, true>(a, grid, st, drop) : launch_fwd<64, false>(a, grid, st, drop);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_attn_fwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
@@ -1137,13 +1198,14 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
   BwdArgs a;
   a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
   a.causal = causal; a.plus_one = plus_one;
+  a.drop_off = sca_drop_offset_ptr();
   const int err = check_common(a, hd, nprob);
   if (err) {
     sca_set_error(err == 2 ? "sca_attn_bwd: head_dim must be 16, 32 or 64"
                            : "sca_attn_bwd: bad shape / leading dimension / causal with Tq != Tk");
     return SCA_ERR_ARG;
   }
-  bool am = false;
+  bool am = false, drop = false;
   for (int i = 0; i < nprob; ++i) {
     const sca_attn_bwd_problem& p = probs[i];
     if (!p.q || !p.k || !p.v || !p.o || !p.dout || !p.stat_m || !p.stat_ll || !p.dq || !p.dk || !p.dv || !p.delta) {
@@ -1159,14 +1221,19 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
       sca_set_error("sca_attn_bwd: all problems must agree on dq_part");
       return SCA_ERR_ARG;
     }
+    if (!(p.drop_p >= 0.f && p.drop_p < 1.f)) {
+      sca_set_error("sca_attn_bwd: drop_p must be in [0, 1)");
+      return SCA_ERR_ARG;
+    }
+    drop = drop || p.drop_p > 0.f;
     a.p[i] = p;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nqb = (Tq + QB - 1) / QB, nkb = (Tk + KB - 1) / KB;  // causal: paired blocks
   dim3 gq(causal ? (nqb + 1) / 2 : nqb, B * H, nprob), gk(causal ? (nkb + 1) / 2 : nkb, B * H, nprob);
-  if (hd == 16) am ? launch_bwd<16, true>(a, gq, gk, st) : launch_bwd<16, false>(a, gq, gk, st);
-  else if (hd == 32) am ? launch_bwd<32, true>(a, gq, gk, st) : launch_bwd<32, false>(a, gq, gk, st);
-  else am ? launch_bwd<64, true>(a, gq, gk, st) : launch_bwd<64, false>(a, gq, gk, st);
+  if (hd == 16) am ? launch_bwd<16, true>(a, gq, gk, st, drop) : launch_bwd<16, false>(a, gq, gk, st, drop);
+  else if (hd == 32) am ? launch_bwd<32, true>(a, gq, gk, st, drop) : launch_bwd<32, false>(a, gq, gk, st, drop);
+  else am ? launch_bwd<64, true>(a, gq, gk, st, drop) : launch_bwd<64, false>(a, gq, gk, st, drop);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_attn_bwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

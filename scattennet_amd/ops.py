@@ -814,7 +814,8 @@ class KeyPaddingMask:
         return self.mask.shape
 
 
-def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v):
+def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
+    """drop: None or (p, seeds) — attention-probability dropout, one seed per problem."""
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
@@ -825,7 +826,8 @@ def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v):
         gs = range(c, min(G, c + L.ATTN_MAX_PROBLEMS))
         arr = (L.AttnFwdProblem * len(gs))(*[
             L.AttnFwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
-                             sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask)) for g in gs])
+                             sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask),
+                             drop[1][g] if drop else 0, drop[0] if drop else 0.0) for g in gs])
         fl = len(gs) * 4.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
         with _timed("attn_fwd_kernel<%d>" % hd, fl):
             L.check(L.lib().sca_attn_fwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
@@ -833,7 +835,8 @@ def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v):
     return o, sm, sl
 
 
-def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, dout, dq_scale=1.0, dv_scale=1.0):
+def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, dout, dq_scale=1.0, dv_scale=1.0,
+              drop=None):
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
@@ -850,7 +853,8 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
             L.AttnBwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
                              dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
                              ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
-                             delta[g].data_ptr(), dq_scale, dv_scale, ptr(part[g])) for g in gs])
+                             delta[g].data_ptr(), dq_scale, dv_scale, ptr(part[g]),
+                             drop[1][g] if drop else 0, drop[0] if drop else 0.0) for g in gs])
         fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
         with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
             L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
@@ -890,7 +894,8 @@ class AttentionBlock(Function):
     into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, kvacc, *ts):
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, kvacc,
+                attn_p, *ts):
         cross = kind == "cross"
         ln = ln_eps is not None  # post-LN LayerNorm fused into the out-projection (sca_gemm_ln)
         if ln:
@@ -930,7 +935,9 @@ class AttentionBlock(Function):
                 probs.append(_prob([_seg(kf, Wk, d, d, d)], k[g], B * Tk, d, d, bias=bk))
                 probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
             gemm(L.GEMM_NT, probs)
-        o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v)
+        # attention-probability dropout (attention.py:67-69): its seeds precede the block's own
+        attn_drop = (attn_p, dropout_seeds(G)) if attn_p > 0 else None
+        o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=attn_drop)
         # v = x + dropout(o Wo^T + bo)  (keypoint_module.py:63-65 / :99-101) in one epilogue,
         # and with `ln` the block's LayerNorm y = LN(v) in the same launch
         seeds = dropout_seeds(G) if drop_p > 0 else [None] * G
@@ -949,6 +956,7 @@ class AttentionBlock(Function):
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
         ctx.kvacc = kvacc if cross else None  # (KvGradAccumulator, index in the chain)
+        ctx.attn_drop = attn_drop
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
         ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, Wo if drop_p == 0 else None) if ln else None
@@ -997,7 +1005,7 @@ class AttentionBlock(Function):
         # dq comes back pre-multiplied by the q scale and dv by alpha_v, so that every GEMM below
         # runs with unit segment scales: dX = dq' Wq + dk Wk + dv' Wv, dWq = dq'^T x, ...
         dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do,
-                               dq_scale=scale, dv_scale=av)
+                               dq_scale=scale, dv_scale=av, drop=ctx.attn_drop)
         # input gradients (residual gradient fused as the epilogue's resid term); with `lnprev`
         # the query input's LayerNorm backward rides in the same launch (sca_gemm_lnb)
         dxq, dxkv, probs, kvprobs = [], [], [], []
@@ -1046,7 +1054,7 @@ class AttentionBlock(Function):
                 acc.buf = None
             else:
                 dxkv = [None] * G
-        return (None,) * 12 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
+        return (None,) * 13 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
             tuple(dbo) + dgam + dbet
 
 

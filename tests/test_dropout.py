@@ -80,6 +80,8 @@ class SeedLog:
 def seedlog():
     from scattennet_amd import ops
     log = SeedLog()
+    if torch.cuda.is_available():  # the oracle replays raw seeds: device step counter at 0
+        ops.dropout_counter().zero_()
     ops._SEED_SOURCE = log
     yield log
     ops._SEED_SOURCE = None
@@ -259,3 +261,84 @@ def test_graph_replays_draw_fresh_masks():
     b = (y == 0).clone()
     torch.cuda.synchronize()
     assert 0.1 < float(a.float().mean()) < 0.3 and not torch.equal(a, b)
+
+
+# --------------------------------------------------------------------------- attention dropout
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,B,Tq,Tk,d,H,explicit", [
+    ("self", 2, 96, 96, 64, 4, False),      # hd 16: the fused single-launch backward
+    ("causal", 2, 80, 80, 64, 4, False),
+    ("cross", 2, 48, 70, 64, 4, False),
+    ("self", 2, 300, 300, 64, 2, False),    # hd 32 beyond one key block: the key-block backward
+    ("causal", 2, 270, 270, 64, 2, False),
+    ("self", 2, 70, 70, 128, 2, False),     # hd 64: split dq / dkdv kernels
+    ("cross", 2, 40, 50, 64, 4, True),      # a materialised additive mask: the general path
+])
+def test_attention_probability_dropout(kind, B, Tq, Tk, d, H, explicit, seedlog):
+    """attention.py:67-69 / 119-121 / 173-175: F.dropout on the softmax probabilities in
+    training mode — forward (O from the dropped probabilities, statistics of the undropped
+    ones) and every gradient against the oracle replaying the HIP path's seed."""
+    import scattennet_amd as S
+    dev = _dev()
+    torch.manual_seed(Tq + Tk)
+    cls = {"self": S.SelfAttention, "causal": S.SelfCausalAttention, "cross": S.CrossAttention}[kind]
+    m = cls(d, H, dropout=0.3)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn_like(p) / (p.shape[-1] ** 0.5 if p.dim() == 2 else 10.0))
+    m = m.to(dev).train()
+    x, kv = torch.randn(B, Tq, d), torch.randn(B, Tk, d)
+    mask = torch.ones(B, Tk, dtype=torch.long)
+    mask[1, Tk // 2:] = 0
+    if kind == "causal":
+        am = O.additive_causal_mask(mask)
+    else:
+        am = O.additive_key_mask(mask, tgt_len=Tq)
+    amask = am.to(dev) if explicit else S.key_padding_mask(mask.to(dev), causal=(kind == "causal"))
+    xg, kvg = x.to(dev).requires_grad_(True), kv.to(dev).requires_grad_(True)
+    out = m(xg, kvg, amask) if kind == "cross" else m(xg, amask)
+    g = torch.randn(out.shape)
+    out.backward(g.to(dev))
+    p = _ref_params(m)
+    xr, kvr = x.clone().requires_grad_(True), kv.clone().requires_grad_(True)
+    ref = O.attention({"a." + k: v for k, v in p.items()}, "a", xr, kvr if kind == "cross" else xr, am, H, kind,
+                      O.Drop(0.3, seedlog.stream(0)))
+    assert len(seedlog.draws) == 1  # one seed per call
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * g).sum().backward()
+    assert rel_err(xg.grad, xr.grad) < PARITY_TOL
+    if kind == "cross":
+        assert rel_err(kvg.grad, kvr.grad) < PARITY_TOL
+    _grads_close(m, p)
+    # dropout actually applied: the eval-mode output differs
+    with torch.no_grad():
+        m.eval()
+        ev = m(xg, kvg, amask) if kind == "cross" else m(xg, amask)
+    assert rel_err(ev, out.detach()) > 1e-2
+
+
+@pytest.mark.gpu
+def test_sca_stack_attention_and_block_dropout(seedlog):
+    """The SCA stack (L = 2) with attention_dropout 0.1 AND the blocks' dropout 0.2: every
+    attention draws its seed before its block's own (the reference's call order)."""
+    import scattennet_amd as S
+    dev = _dev()
+    fx = load("sca_L2")
+    cfg = dict(fx["meta"]["cfg"], dropout=0.2, attention_dropout=0.1)
+    m = S.SeparativeCoordinateAttention(cfg)
+    m.load_state_dict(fx["param"])
+    m = m.to(dev).train()
+    xe = fx["in"]["x_embed"].to(dev).requires_grad_(True)
+    ye = fx["in"]["y_embed"].to(dev).requires_grad_(True)
+    out = m(xe, ye, fx["in"]["mask"].to(dev))
+    out.backward(fx["gout"].to(dev))
+    p = _ref_params(m)
+    xr = fx["in"]["x_embed"].clone().requires_grad_(True)
+    yr = fx["in"]["y_embed"].clone().requires_grad_(True)
+    seeds = iter(seedlog.stream(0))  # one stream of seeds shared by both dropout kinds
+    ref = O.sca(p, "", xr, yr, fx["in"]["mask"], cfg, drop=O.Drop(0.2, seeds), attn_drop=O.Drop(0.1, seeds))
+    assert next(seeds, None) is None  # every seed the HIP path drew was used
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * fx["gout"]).sum().backward()
+    assert rel_err(xe.grad, xr.grad) < PARITY_TOL and rel_err(ye.grad, yr.grad) < PARITY_TOL
+    _grads_close(m, p)
