@@ -439,6 +439,16 @@ int sca_coord_map_bwd(int nprob, const sca_coord_map_bwd_problem* probs, int row
  * longer side and squared, clamped to [0, 1], then x, y mapped into it (an axis whose
  * clamped extent is 0 is left as is).  Frames t >= lengths[b] are written as zeros (the
  * collator's padding, dataset.py:82-91).  K_all <= 1024; kp_out may alias kp_in.        */
+/* The sample pipeline of SLR_Dataset.data_collator for a batch in one launch
+ * (dataset.py:58-125 with preprocess_keypoints :124-132): for t < lengths[b], frame (b, t)
+ * is raw row src_row[b T + t] (frame selection, dataset.py:185-215, decided on the host with
+ * the reference's RNG calls), transformed by the clip's augmentation affine (affine + 6 b =
+ * [a00 a01 tx a10 a11 ty]: rotation about (0, 0) and / or x -> 1 - x, augmentation.py:3-25;
+ * NULL = none) and then normalised as sca_normalize_parts (nparts = 0: not normalised);
+ * frames t >= lengths[b] are zeros.  raw: (R, K_all, 2) fp32, all clips' frames.          */
+int sca_prepare_keypoints(const float* raw, const int* src_row, const float* affine, const int* lengths,
+                          float* kp_out, int B, int T, int K_all, const int* part_off, const int* part_idx,
+                          int nparts, void* stream);
 int sca_normalize_parts(const float* kp_in, float* kp_out, const int* lengths, int B, int T, int K_all,
                         const int* part_off, const int* part_idx, int nparts, void* stream);
 

@@ -141,6 +141,7 @@ EXPORTS = {
     "sca_coord_map_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_coord_map_bwd_chunks": ([c_int], c_int),
     "sca_coord_map_bwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "sca_prepare_keypoints": ([c_void_p] * 5 + [c_int] * 3 + [c_void_p, c_void_p, c_int, c_void_p], c_int),
     "sca_normalize_parts": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                              c_void_p], c_int),
     "sca_ctc_workspace_floats": ([c_int, c_int, c_int], c_long),

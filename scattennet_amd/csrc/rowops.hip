@@ -547,6 +547,8 @@ struct NormArgs {
   const int* part_off;
   const int* part_idx;
   int B, T, K_all, nparts;
+  const int* src_row;   // prepare: row of `in` holding frame (b, t) (frame selection), or NULL: in is (B, T, ...)
+  const float* affine;  // prepare: per clip [a00 a01 tx a10 a11 ty] (augmentation), or NULL
 };
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -562,14 +564,26 @@ __global__ __launch_bounds__(256) void normalize_parts_kernel(const NormArgs a) 
   if (frame >= (long)a.B * a.T) return;
   const int b = (int)(frame / a.T), t = (int)(frame % a.T);
   const int n2 = 2 * a.K_all;
-  const float* src = a.in + frame * n2;
   float* dst = a.out + frame * n2;
   if (t >= a.lengths[b]) {  // collator padding
     for (int e = lane; e < n2; e += 64) dst[e] = 0.f;
     return;
   }
+  // frame selection (dataset.py:185-215): the selected source row; augmentation
+  // (dataset.py:172-183, augmentation.py): x' = a00 x + a01 y + tx, y' = a10 x + a11 y + ty
+  const float* src = a.in + (a.src_row ? (long)a.src_row[frame] : frame) * n2;
   float* F = fr[w];
-  for (int e = lane; e < n2; e += 64) F[e] = src[e];
+  if (a.affine) {
+    const float* m = a.affine + 6 * b;
+    const float a00 = m[0], a01 = m[1], tx = m[2], a10 = m[3], a11 = m[4], ty = m[5];
+    for (int k = lane; k < a.K_all; k += 64) {
+      const float x = src[2 * k], y = src[2 * k + 1];
+      F[2 * k] = fmaf(a00, x, fmaf(a01, y, tx));
+      F[2 * k + 1] = fmaf(a10, x, fmaf(a11, y, ty));
+    }
+  } else {
+    for (int e = lane; e < n2; e += 64) F[e] = src[e];
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -897,9 +911,26 @@ extern "C" int sca_normalize_parts(const float* kp_in, float* kp_out, const int*
   }
   const long frames = (long)B * T;
   if (frames == 0) return SCA_OK;
-  NormArgs a{kp_in, kp_out, lengths, part_off, part_idx, B, T, K_all, nparts};
+  NormArgs a{kp_in, kp_out, lengths, part_off, part_idx, B, T, K_all, nparts, nullptr, nullptr};
   hipLaunchKernelGGL(normalize_parts_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_normalize_parts: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_prepare_keypoints(const float* raw, const int* src_row, const float* affine, const int* lengths,
+                                     float* kp_out, int B, int T, int K_all, const int* part_off, const int* part_idx,
+                                     int nparts, void* stream) {
+  if (B < 0 || T < 0 || K_all < 1 || K_all > NORM_KMAX || nparts < 0 || !raw || !src_row || !kp_out || !lengths ||
+      (nparts > 0 && (!part_off || !part_idx)) || raw == kp_out) {
+    sca_set_error("sca_prepare_keypoints: bad arguments (K_all must be 1..1024; raw must not alias kp_out)");
+    return SCA_ERR_ARG;
+  }
+  const long frames = (long)B * T;
+  if (frames == 0) return SCA_OK;
+  NormArgs a{raw, kp_out, lengths, part_off, part_idx, B, T, K_all, nparts, src_row, affine};
+  hipLaunchKernelGGL(normalize_parts_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_prepare_keypoints: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
