@@ -314,5 +314,6 @@ def test_sca_stack_kv_gradient_accumulated_in_epilogue(monkeypatch):
         ((out["outputs"] * g1).sum() + (out["self_attn_map"] * g2).sum()).backward()
         torch.cuda.synchronize()
         grads.append([xg.grad.clone(), yg.grad.clone()] + [p.grad.clone() for p in m.parameters()])
-    for a, b in zip(*grads):
-        assert rel_err(b, a) < 1e-5
+    gscale = max(float(t.abs().max()) for t in grads[0])
+    for a, b in zip(*grads):  # (analytically-zero gradients, e.g. the key bias: both at noise level)
+        assert close(b.cpu(), a.cpu(), 1e-5, gscale), rel_err(b, a)
