@@ -109,9 +109,18 @@ __device__ __forceinline__ f32x4 row_frag(const float* img, int row, int slot) {
   return ld4(img + row * HD + 4 * (slot ^ row_swz<HD>(row)));
 }
 
+// float4-slot swizzle of row d in a transposed [HD][64] image.  Bits 1-3 carry d >> 2 so
+// that the ds_write_b32 transposes of store_cols (32-lane groups, banks mod 32) are
+// conflict-free at hd 16 and bits 0/3 carry d & 3 so that the 16-lane ds_read_b128 groups of
+// col_frag stay conflict-free (MI355X_MICROARCH.md §LDS lane groups; hd 32/64 keep 2-way
+// store conflicts instead of the 8-way of a d & 7 swizzle)
+__device__ __forceinline__ int col_swz(int d) {
+  return (((d >> 2) << 1) | (d & 1) | ((d & 2) << 2)) & 15;
+}
+
 // transposed image [HD][64]: 4 consecutive keys/queries at float4 slot `slot` of row d
 __device__ __forceinline__ f32x4 col_frag(const float* img, int d, int slot) {
-  return ld4(img + d * 64 + 4 * (slot ^ (2 * (d & 7))));
+  return ld4(img + d * 64 + 4 * (slot ^ col_swz(d)));
 }
 
 template <int HD>
@@ -144,7 +153,7 @@ __device__ __forceinline__ void store_cols(float* img, const f32x4* r) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int d = c + j;
-      img[d * 64 + 4 * ((row >> 2) ^ (2 * (d & 7))) + (row & 3)] = r[i][j];
+      img[d * 64 + 4 * ((row >> 2) ^ col_swz(d)) + (row & 3)] = r[i][j];
     }
   }
 }
@@ -167,7 +176,7 @@ __device__ __forceinline__ TileId xcd_tile() {
 
 // ------------------------------------------------------------------------------ forward
 template <int HD, bool ADDMASK, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const FwdArgs a) {
   constexpr int NS = HD / 4;   // MFMA k-steps over the head dim
   constexpr int ND = HD / 16;  // 16-wide output d-blocks
   constexpr int RV = Blk<HD>::RV;
@@ -238,6 +247,23 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
     const int kb = blk * KB, buf = blk & 1;
     const bool more = blk + 1 < nblk;
     float sv[4][4];
+    // the four key tiles' S chains are interleaved k-step by k-step: independent
+    // accumulators keep the MFMA pipe busy instead of waiting out each chain's latency
+    f32x4 sacc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) sacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; s += 4) {
+      f32x4 kv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (!(DIAG && t > w)) kv[t] = row_frag<HD>(Ks[buf], 16 * t + qi, (NS * grp + s) >> 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (!(DIAG && t > w)) sacc[t] = mfma16(kv[t][j], qreg[s + j], sacc[t]);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (DIAG && t > w) {  // wave-uniform: the whole tile is above the diagonal
@@ -245,13 +271,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
         for (int r = 0; r < 4; ++r) sv[t][r] = -INFINITY;
         continue;
       }
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NS; s += 4) {
-        const f32x4 kv = row_frag<HD>(Ks[buf], 16 * t + qi, (NS * grp + s) >> 2);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = mfma16(kv[j], qreg[s + j], acc);
-      }
+      const f32x4 acc = sacc[t];
       const int kl = 16 * t + 4 * grp;
       const f32x4 ad = ld4(&Ka[buf][kl]);
 #pragma unroll
@@ -274,15 +294,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const FwdArgs a) {
     const float m_new = fmaxf(m_run, mloc);  // finite after block 0 (key 0 is always in the row)
     const float alpha = fast_exp2(m_run - m_new);
     m_run = m_new;
-    float psum = 0.f;
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};  // 4 partial sums: short dependent add chains
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = fast_exp2(sv[t][r] - m_new);
-        psum += p;  // the row sum (softmax statistics) of the undropped probabilities
+        ps[r] += p;  // the row sum (softmax statistics) of the undropped probabilities
         sv[t][r] = DROP ? dm.apply(erow + (uint32_t)(kb + 16 * t + 4 * grp + r), p) : p;
       }
+    const float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
     l_run = l_run * alpha + psum;
 #pragma unroll
     for (int d = 0; d < ND; ++d) o[d] *= alpha;
