@@ -641,25 +641,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
 //   wave w owns the key tiles g = 4i + w (i < 4; 16 keys each, interleaved so that the
 //   causal triangle gives every wave the same work): K / V rows and the K^T fragments of
 //   them in registers;
-//   per 64-query block (Q, dO, their transposes and the row stats staged in LDS, double-
-//   buffered one block ahead, delta = rowsum(dO * O) computed at staging), for each
-//   (query tile t, own key tile g): S = Q K^T, dP = dO V^T (key on the lane),
+//   per 64-query block (Q, dO, their transposes and the row stats staged in LDS; the next
+//   block's loads are issued at the top and consumed — delta = rowsum(dO * O) included — only
+//   when it is committed at the end, so their latency hides under the block's tiles), for
+//   each (query tile t, own key tile g): S = Q K^T, dP = dO V^T (key on the lane),
 //     P = exp2(S log2e + add - m - ll), dS = P (dP - delta), dV += dO^T P, dK += Q^T dS,
 //     dS transposed through a wave-private LDS tile (padded rows: conflict-free), and
 //     dQ_w += dS K over the wave's own keys;
 //   the four waves' dQ partials are summed in fixed order through LDS (deterministic).
-// ~55 KB of LDS: two workgroups per CU.
+// One staging buffer (the next block is committed after the barrier that ends every wave's
+// reads of the current one and before the barrier that opens the next): 38 KB of LDS, so
+// the register file (186-226 VGPRs: two waves per SIMD) sets the occupancy, and co-running
+// kernels keep LDS room on the CU.
 constexpr int FB_TMAX = 256;
 constexpr int FB_TS = 20;  // row stride of the 16x16 dS transposition tile (16 + 4 pad)
+constexpr int FB_NB = 1, FB_OCC = 2;
 
 template <bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a) {
+__global__ __launch_bounds__(256, FB_OCC) void attn_bwd_fused_kernel(const BwdArgs a) {
   constexpr int HD = 16, NS = 4;
-  __shared__ __attribute__((aligned(16))) float Qs[2][QB * HD];
-  __shared__ __attribute__((aligned(16))) float Ds[2][QB * HD];
-  __shared__ __attribute__((aligned(16))) float Qt[2][HD * QB];
-  __shared__ __attribute__((aligned(16))) float Dt[2][HD * QB];
-  __shared__ __attribute__((aligned(16))) float Sm[2][QB], Sl[2][QB], Sd[2][QB];
+  __shared__ __attribute__((aligned(16))) float Qs[FB_NB][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Ds[FB_NB][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Qt[FB_NB][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Dt[FB_NB][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Sm[FB_NB][QB], Sl[FB_NB][QB], Sd[FB_NB][QB];
   __shared__ __attribute__((aligned(16))) float dSw[4][16 * FB_TS];
   __shared__ __attribute__((aligned(16))) float dQr[4][QB * HD];
 
@@ -702,35 +707,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
   const float* qbase = P.q + (long)b * Tq * a.ldq + h * HD;
   const float* dbase = P.dout + (long)b * Tq * a.ldo + h * HD;
   const float* obase = P.o + (long)b * Tq * a.ldo + h * HD;
-  f32x4 rq[1], rd[1];
-  float cm = 0.f, cl = 0.f, cdel = 0.f;
+  // prefetch only issues the loads (in flight during the block's tiles); everything that
+  // consumes them — delta = rowsum(dO * O), the past-the-end rows' stats — waits for commit
+  f32x4 rq[1], rd[1], ro[1];
+  float cm = 0.f, cl = 0.f;
   int qbn = 0;
   auto prefetch = [&](int q0) {
     blk_load<HD>(rq, qbase, a.ldq, q0, Tq);
     blk_load<HD>(rd, dbase, a.ldo, q0, Tq);
-    f32x4 ro[1];
     blk_load<HD>(ro, obase, a.ldo, q0, Tq);
-    // delta of row (threadIdx.x >> 2): 4 consecutive lanes hold its 16 dO*O products
-    float dp = rd[0][0] * ro[0][0] + rd[0][1] * ro[0][1] + rd[0][2] * ro[0][2] + rd[0][3] * ro[0][3];
-    dp += __shfl_xor(dp, 1, 64);
-    dp += __shfl_xor(dp, 2, 64);
-    cdel = dp;
     if (threadIdx.x < QB) {
-      const int q = q0 + threadIdx.x;
-      const long si = ((long)b * a.H + h) * Tq + min(q, Tq - 1);
+      const long si = ((long)b * a.H + h) * Tq + min(q0 + (int)threadIdx.x, Tq - 1);
       cm = P.stat_m[si];
       cl = P.stat_ll[si];
-      if (q >= Tq) cm = INFINITY;  // rows past the end: p = exp2(-inf) = 0
     }
     qbn = q0;
   };
   auto commit = [&](int buf) {
+    // delta of row (threadIdx.x >> 2): 4 consecutive lanes hold its 16 dO*O products
+    float cdel = rd[0][0] * ro[0][0] + rd[0][1] * ro[0][1] + rd[0][2] * ro[0][2] + rd[0][3] * ro[0][3];
+    cdel += __shfl_xor(cdel, 1, 64);
+    cdel += __shfl_xor(cdel, 2, 64);
     store_rows<HD>(Qs[buf], rq);
     store_cols<HD>(Qt[buf], rq);
     store_rows<HD>(Ds[buf], rd);
     store_cols<HD>(Dt[buf], rd);
     if (threadIdx.x < QB) {
-      Sm[buf][threadIdx.x] = cm;
+      Sm[buf][threadIdx.x] = qbn + (int)threadIdx.x < Tq ? cm : INFINITY;  // past the end: p = 0
       Sl[buf][threadIdx.x] = cl;
     }
     if ((threadIdx.x & 3) == 0) {
@@ -745,7 +748,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
 
 #pragma unroll 1
   for (int qb = 0; qb < nqb; ++qb) {
-    const int buf = qb & 1;
+    const int buf = qb % FB_NB;
     __syncthreads();  // block qb staged; the previous block's dQ partials consumed
     if (qb + 1 < nqb) prefetch((qb + 1) * QB);  // in flight during this block
 #pragma unroll
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused_kernel(const BwdArgs a)
       const f32x4 s = ((ld4(&dQr[0][e]) + ld4(&dQr[1][e])) + ld4(&dQr[2][e])) + ld4(&dQr[3][e]);
       st4(P.dq + ((long)b * Tq + qrow) * a.ldq + h * HD + 4 * grp, s * P.dq_scale);
     }
-    if (qb + 1 < nqb) commit(buf ^ 1);
+    if (qb + 1 < nqb) commit((qb + 1) % FB_NB);
   }
 
 #pragma unroll
