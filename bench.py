@@ -202,6 +202,17 @@ def main():
         if tr:
             roofline["traffic"] = round(tr["bytes_per_launch"])
             roofline["traffic_source"] = "profiles/traffic_latest.json (rocprofv3 PMC, bytes per launch)"
+    # the same kernel's average duration from the committed rocprofv3 kernel-trace stats of
+    # this command (profiles/kstats_latest.csv): the profiler-side figure beside the event one
+    kpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "kstats_latest.csv")
+    if os.path.exists(kpath):
+        import csv
+        for r in csv.DictReader(open(kpath)):
+            if r["Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0] == kname:
+                avg_s = float(r["AverageNs"]) * 1e-9
+                roofline["rocprof_avg_launch_us"] = round(avg_s * 1e6, 2)
+                roofline["rocprof_frac"] = round(roofline["flops_per_launch"] / avg_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
+                roofline["rocprof_source"] = "profiles/kstats_latest.csv (rocprofv3 --kernel-trace --stats)"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not fusion and args.dropout == 0:
