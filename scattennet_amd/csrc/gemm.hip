@@ -601,11 +601,6 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
     if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
     const char* As = smem + (t % S) * STAGE;
     const char* Bs = As + GL_OP_BYTES;
-    if (do_bias && threadIdx.x < GL_BM) {
-      const float* af = (const float*)As;  // TN: A image is [32 k][64 m]
-#pragma unroll 8
-      for (int k = 0; k < GL_BK; ++k) bsum += af[k * 64 + threadIdx.x];
-    }
     f32x4 fa[4], fb[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -616,18 +611,29 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
+    // bias gradient (TN: colsum of dY = the A tile's row sums) from the A fragments already
+    // in registers: waves 0 and 2 hold rows wm .. wm+31, a lane k = 8g + 4h + j of its row
+    // (the two half-waves' partials are combined after the loop).  Earlier form: wave 0
+    // re-read the whole A image from LDS every slice (4 LDS round trips + a serial add
+    // chain), which made the bias tiles the launch's slowest workgroups.
+    if (do_bias && (wave & 1) == 0) {
+      f32x4 s4 = (fa[0] + fa[1]) + (fa[2] + fa[3]);
+      bsum += (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    }
   }
 
   const float alpha = P.seg[0].alpha;
   const bool fused_k = splitk > 1 && args.counters != nullptr;  // in-launch split-K combine
-  if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
-    float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m0 + threadIdx.x;
+  if (do_bias) bsum += __shfl_xor(bsum, 32, 64);  // the two k halves of a row
+  const int brow = wm + lane;                     // this lane's bias row (waves 0, 2; lanes < 32)
+  if (do_bias && (wave & 1) == 0 && lane < 32 && m0 + brow < P.M) {
+    float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m0 + brow;
     if (fused_k)
       __hip_atomic_store(bp, bsum * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
     else if (splitk > 1)
       *bp = bsum * alpha;
     else
-      P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
+      P.bias_grad[m0 + brow] = bsum * alpha * P.bias_grad_scale;
   }
   if (alpha != 1.f) {
 #pragma unroll

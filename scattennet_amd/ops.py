@@ -362,8 +362,17 @@ def _next_of(xs):
     return [getattr(x, "_sca_next", None) for x in xs]
 
 
+# Chained passes only when the launch has a 32-row tile for every CU: the passes run at one
+# workgroup per tile, so a launch of a few tiles would do them on a few CUs
+# (tools/gemm_ln_bench.py, 1 x (2048, 256, 256) + fc1: 52.8 us chained vs 28.4 us as a
+# separate 64x64-tile GEMM); the consumer then computes its projections itself
+_CHAIN_MIN_TILES = int(__import__("os").environ.get("SCA_CHAIN_MIN_TILES", "256"))
+
+
 def _chain_lns(nxt, G, M, like, gam, bet, ys, means, rstds):
     """GemmLnProblems of a fused GEMM + LayerNorm launch, with `nxt`'s chained passes."""
+    if nxt is not None and G * ((M + 31) // 32) < _CHAIN_MIN_TILES:
+        nxt = None
     lns = []
     for g in range(G):
         ps = nxt.passes(g, M, like) if nxt is not None else []

@@ -251,6 +251,7 @@ def test_sca_stack_chained_projections_vs_oracle(chain, monkeypatch):
     from scattennet_amd import _lib as L, ops
     from scattennet_amd.workloads import model_cfg
     monkeypatch.setattr(ops, "_CHAIN_NEXT", chain)
+    monkeypatch.setattr(ops, "_CHAIN_MIN_TILES", 0)  # chain even at this test's 8 row tiles
     dev = torch.device("cuda:0")
     torch.manual_seed(21)
     B, T, d, H = 3, 80, 256, 16

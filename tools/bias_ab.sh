@@ -1,0 +1,9 @@
+# GPU call: full GPU suite, then in-step A/B of the in-tree library vs libscatten_hip_prev.so,
+# then an env-toggle sweep (args) on config 2
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+STEPS=100 bash tools/ab_lib.sh || exit 1
+STEPS=100 REPS=2 bash tools/env_ab.sh "$@"
