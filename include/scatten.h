@@ -164,6 +164,10 @@ typedef struct {
 
 int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                 void* stream);
+/* Row-tile height (32 or 16) sca_gemm_ln launches for nprob problems of at most maxM rows,
+ * chained passes or not — the rule the launcher applies (SCA_GEMM_LN_BM overrides without
+ * chained passes); hosts use it to name the kernel variant in their profiles. */
+int sca_gemm_ln_rows(int nprob, int maxM, int chain);
 
 /* NN input-gradient GEMM + the backward of the LayerNorm that produced its input, in one
  * launch (d_model = 256).  Per problem:

@@ -121,6 +121,7 @@ EXPORTS = {
     "sca_gemm_splitk_counters": ([c_int, c_int, c_int], c_long),
     "sca_gemm_splitk_fused": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
+    "sca_gemm_ln_rows": ([c_int, c_int, c_int], c_int),
     "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_lnb_blocks": ([c_int], c_int),
     "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),

@@ -1928,6 +1928,17 @@ extern "C" int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_probl
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, true, counters);
 }
 
+// 32-row tiles (8 waves) whenever they give a workgroup per CU, else 16-row tiles (2
+// workgroups / CU): tools/gemm_ln_bench.py 4x(2048,256,K): K = 768 41.0 vs 44.6 us,
+// K = 256 19.8 vs 20.8 us; 1x(2048,256,256): 15.2 vs 10.9 us.  Chained passes: always 32.
+extern "C" int sca_gemm_ln_rows(int nprob, int maxM, int chain) {
+  static const int bm_env = getenv("SCA_GEMM_LN_BM") ? atoi(getenv("SCA_GEMM_LN_BM")) : 0;
+  const long wg32 = (long)nprob * ((maxM + 31) / 32);
+  if (chain) return 32;
+  if (bm_env == 16 || bm_env == 32) return bm_env;
+  return wg32 >= 256 ? 32 : 16;
+}
+
 extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                            void* stream) {
   if (nprob <= 0) return SCA_OK;
@@ -1980,13 +1991,7 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
     maxM = maxM > P.M ? maxM : P.M;
   }
   if (maxM == 0) return SCA_OK;
-  // 32-row tiles (8 waves) whenever they give a workgroup per CU, else 16-row tiles (2
-  // workgroups / CU): tools/gemm_ln_bench.py 4x(2048,256,K): K = 768 41.0 vs 44.6 us,
-  // K = 256 19.8 vs 20.8 us; 1x(2048,256,256): 15.2 vs 10.9 us
-  static const int bm_env = getenv("SCA_GEMM_LN_BM") ? atoi(getenv("SCA_GEMM_LN_BM")) : 0;
-  const long wg32 = (long)nprob * ((maxM + 31) / 32);
-  // (chained passes: always the 32-row tile)
-  const int bm = chain ? 32 : bm_env ? bm_env : (wg32 >= 256 ? 32 : 16);
+  const int bm = sca_gemm_ln_rows(nprob, maxM, chain);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (chain) {
     hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);

@@ -253,9 +253,35 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(const ReduceArgs a) {
   }
 }
 
+// Few rows (S <= 16, e.g. the position-table gradient: the sum over the B clips of a
+// (T, N) gradient): one thread per float4 column, the S rows summed in order — the same
+// order, and so the same bits, as reduce_rows_kernel gives for S <= RED_WAVES (wave w holds
+// row w alone; the wave partials are added in order); the 16-wave form left most waves
+// idle and needed I x N/64 workgroups of 1024 threads.
+__global__ __launch_bounds__(256) void reduce_rows_few_kernel(const ReduceArgs a) {
+  const sca_reduce_problem& P = a.p[blockIdx.z];
+  const int j = 4 * (blockIdx.x * 256 + threadIdx.x);
+  if (j >= a.N) return;
+  const float* base = P.in + (long)blockIdx.y * a.stride_i + j;
+  f32x4 t = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < a.S; ++s) t += ld4(base + (long)s * a.stride_s);
+  t *= P.scale;
+  float* o = P.out + (long)blockIdx.y * a.N + j;
+  if (a.accumulate) t += ld4(o);
+  st4(o, t);
+}
+
 int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
-  dim3 grid((a.N + 63) / 64, a.I, nprob);
-  hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(1024), 0, st, a);
+  bool few = a.S <= RED_WAVES && (a.N & 3) == 0 && (a.stride_s & 3) == 0 && (a.stride_i & 3) == 0;
+  for (int i = 0; few && i < nprob; ++i)
+    few = !((reinterpret_cast<uintptr_t>(a.p[i].in) | reinterpret_cast<uintptr_t>(a.p[i].out)) & 15);
+  if (few) {
+    dim3 grid((a.N / 4 + 255) / 256, a.I, nprob);
+    hipLaunchKernelGGL(reduce_rows_few_kernel, grid, dim3(256), 0, st, a);
+  } else {
+    dim3 grid((a.N + 63) / 64, a.I, nprob);
+    hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(1024), 0, st, a);
+  }
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -419,12 +445,24 @@ __global__ __launch_bounds__(256) void coord_map_fwd_kernel(const MapArgs a) {
     for (int r = 0; r < MAP_ROWS; ++r) ax[r] = ay[r] = 0.f;
     const float* wxr = P.wx + (long)n * K;
     const float* wyr = P.wy + (long)n * K;
-    for (int k = 0; k < K; ++k) {
-      const float wx = wxr[k], wy = wyr[k];
+    // the weight row (K floats, no float4 alignment) in chunks of 8 loads issued together:
+    // one L2 round trip per 8 joints instead of one per joint (same k order: bit-identical)
+    for (int k0 = 0; k0 < K; k0 += 8) {
+      float wx[8], wy[8];
 #pragma unroll
-      for (int r = 0; r < MAP_ROWS; ++r) {
-        ax[r] = fmaf(xs[r][k], wx, ax[r]);
-        ay[r] = fmaf(ys[r][k], wy, ay[r]);
+      for (int j = 0; j < 8; ++j) {
+        const int k = min(k0 + j, K - 1);
+        wx[j] = wxr[k];
+        wy[j] = wyr[k];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (k0 + j >= K) break;  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < MAP_ROWS; ++r) {
+          ax[r] = fmaf(xs[r][k0 + j], wx[j], ax[r]);
+          ay[r] = fmaf(ys[r][k0 + j], wy[j], ay[r]);
+        }
       }
     }
     const float bx = P.bx ? P.bx[n] : 0.f, by = P.by ? P.by[n] : 0.f;
@@ -439,7 +477,7 @@ __global__ __launch_bounds__(256) void coord_map_fwd_kernel(const MapArgs a) {
   }
 }
 
-// Partial weight gradients: partial[c][chunk][n][k] = sum_{rows in chunk} d{x,y}e[row][n] * {x,y}[row][k]
+// Partial weight gradients: partial[c][chunk][k][n] = sum_{rows in chunk} d{x,y}e[row][n] * {x,y}[row][k]
 // A thread owns one column n: the chunk's 2 x MAP_CHUNK gradient values are loaded into
 // registers up front (one round of loads in flight, not one dependent load per row), then
 // every joint's dot product runs out of registers and the LDS coordinates.
@@ -466,8 +504,9 @@ __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a
       dx[r] = r < nr ? P.dxe[off] : 0.f;
       dy[r] = r < nr ? P.dye[off] : 0.f;
     }
-    float* px = P.partial + ((long)blockIdx.x * a.N + n) * K;
-    float* py = P.partial + ((long)(a.nchunk + blockIdx.x) * a.N + n) * K;
+    // partial layout [chunk][k][n]: the lanes' stores (consecutive n) are coalesced
+    float* px = P.partial + (long)blockIdx.x * a.N * K + n;
+    float* py = P.partial + (long)(a.nchunk + blockIdx.x) * a.N * K + n;
     for (int kc = 0; kc < K; kc += KC) {
       float gx[KC], gy[KC];
 #pragma unroll
@@ -487,8 +526,8 @@ __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
         if (kc + j < K) {
-          px[kc + j] = gx[j];
-          py[kc + j] = gy[j];
+          px[(long)(kc + j) * a.N] = gx[j];
+          py[(long)(kc + j) * a.N] = gy[j];
         }
       }
     }
@@ -499,7 +538,7 @@ __global__ __launch_bounds__(256) void coord_map_bwd_w_kernel(const MapBwdArgs a
 __global__ __launch_bounds__(256) void coord_map_reduce_kernel(const MapBwdArgs a) {
   const sca_coord_map_bwd_problem& P = a.p[blockIdx.z];
   const long NK = (long)a.N * P.K;
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // partial index k * N + n (coalesced reads)
   if (e >= NK) return;
   const float* src = P.partial + (long)blockIdx.y * a.nchunk * NK + e;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -509,7 +548,8 @@ __global__ __launch_bounds__(256) void coord_map_reduce_kernel(const MapBwdArgs 
     for (int u = 0; u < 4; ++u) acc[u] += src[(long)(c + u) * NK];
   }
   for (; c < a.nchunk; ++c) acc[0] += src[(long)c * NK];
-  (blockIdx.y ? P.dwy : P.dwx)[e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  const long k = e / a.N, n = e % a.N;
+  (blockIdx.y ? P.dwy : P.dwx)[n * P.K + k] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 // Keypoint gradients (only when the keypoints require grad): one wave per row.

@@ -236,10 +236,9 @@ def gemm_ln(probs, lns, eps):
         larr = (L.GemmLnProblem * len(lchunk))(*lchunk)
         flops = sum(2.0 * p.M * p.N * (p.seg[0].K + 256 * ln.npass) for p, ln in zip(chunk, lchunk)) \
             if _PROFILER else 0.0
-        # the variant sca_gemm_ln picks (gemm.hip), for the kernel name rocprofv3 shows
+        # the variant sca_gemm_ln picks, for the kernel name rocprofv3 shows
         chain = any(ln.npass > 0 for ln in lchunk)
-        bm = 32 if chain else int(__import__("os").environ.get("SCA_GEMM_LN_BM", "0")) or (
-            32 if len(chunk) * ((max(p.M for p in chunk) + 31) // 32) >= 256 else 16)
+        bm = lib.sca_gemm_ln_rows(len(chunk), max(p.M for p in chunk), int(chain))
         with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}>", flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
@@ -810,7 +809,9 @@ class KeyPaddingMask:
             raise ValueError("key padding mask must be (B, T)")
         self.mask = mask
         self.causal_plus_one = causal_plus_one
-        self.key_valid = (mask != 0).to(torch.float32).contiguous()
+        # one comparison kernel writing fp32 directly (the `!= 0` then `.to` pair was two launches)
+        self.key_valid = torch.empty(mask.shape, dtype=torch.float32, device=mask.device)
+        torch.ne(mask, 0, out=self.key_valid)
 
     def causal_view(self):
         """The causal variant (create_causal_attention_mask) sharing this key-validity vector."""
