@@ -205,7 +205,7 @@ def main():
     # the same kernel's average duration from the committed rocprofv3 kernel-trace stats of
     # this command (profiles/kstats_latest.csv): the profiler-side figure beside the event one
     kpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "kstats_latest.csv")
-    if os.path.exists(kpath):
+    if os.path.exists(kpath) and args.workload == "cfg2" and args.dropout == 0:  # the profiled command
         import csv
         for r in csv.DictReader(open(kpath)):
             if r["Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0] == kname:

@@ -203,6 +203,11 @@ typedef struct {
   const float* aux;   /* NULL, or [M, 256 * npass]: dout *= gelu'(aux) (exact-erf GELU) */
   int npass;          /* 1..3 (0 reads as 1) */
   int ldw;            /* row stride of wo, dout and aux (0 reads as 256 * npass) */
+  /* optional position table (NULL = none): the LayerNorm input is x + tab[(row % tab_T) + 2]
+   * — the embedding LayerNorm of keypoint_module.py:154-160 (x = the mapped coordinates,
+   * tab = LearningPositionEmbedding.weight [>= tab_T + 2, 256], layers.py:15-30)          */
+  const float* tab;
+  int tab_T;
 } sca_gemm_lnb_problem;
 
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);

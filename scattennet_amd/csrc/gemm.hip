@@ -1249,6 +1249,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   for (int i = 0; i < RPW; ++i) {
     const int m = min(m0 + RPW * wave + i, P.M - 1);
     xin[i] = ld4(LN.x + (long)m * LG_BN + n);
+    if (LN.tab) xin[i] += ld4(LN.tab + (long)(m % LN.tab_T + 2) * LG_BN + n);  // v = x + P[t + 2]
     // (no residual: a harmless read of gamma, unused — keeps the loads branch-free)
     rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
     mu[i] = LN.mean[m];
@@ -2021,7 +2022,8 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
     bool ok = P.nseg >= 1 && P.nseg <= SCA_GEMM_MAX_SEGS && P.N == LG_BN && P.M >= 0 && P.C && L.x && L.mean &&
               L.rstd && L.gamma && L.dx && L.partial && P.epi == 0 && !P.bias && !P.bias_grad &&
               P.post_scale == 1.f && (P.ldc & 3) == 0 && P.ldc >= LG_BN &&
-              (!P.resid || ((P.ldr & 3) == 0 && P.ldr >= LG_BN));
+              (!P.resid || ((P.ldr & 3) == 0 && P.ldr >= LG_BN)) &&
+              (!L.tab || (L.tab_T >= 1 && !(reinterpret_cast<uintptr_t>(L.tab) & 15)));
     uintptr_t al = reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
                    reinterpret_cast<uintptr_t>(L.x) | reinterpret_cast<uintptr_t>(L.gamma) |
                    reinterpret_cast<uintptr_t>(L.dx) | reinterpret_cast<uintptr_t>(L.wo) |

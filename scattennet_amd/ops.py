@@ -256,11 +256,12 @@ class LnSaved:
     (`dout`) when no dropout sits between: an attention block's out-projection weight (dO =
     dL/dv Wo) or an FFN's fc2 weight with `aux` = the fc1 pre-activation (dz = (dL/dv W2) *
     gelu'(aux))."""
-    __slots__ = ("v", "mean", "rstd", "gamma", "handoff", "wo", "aux")
+    __slots__ = ("v", "mean", "rstd", "gamma", "handoff", "wo", "aux", "tab", "T")
 
-    def __init__(self, v, mean, rstd, gamma, wo=None, aux=None):
+    def __init__(self, v, mean, rstd, gamma, wo=None, aux=None, tab=None, T=0):
         self.v, self.mean, self.rstd, self.gamma, self.handoff, self.wo = v, mean, rstd, gamma, None, wo
         self.aux = aux
+        self.tab, self.T = tab, T  # position-table mode: the LN input is v + tab[t + 2]
 
 
 def ln_saved_of(ts):
@@ -272,6 +273,8 @@ def ln_saved_of(ts):
 
 
 _CHAIN_DO = __import__("os").environ.get("SCA_CHAIN_DO", "1") != "0"
+# the embedding LayerNorm (position-table mode) handed to its consumer's sca_gemm_lnb
+_EMB_LNB = __import__("os").environ.get("SCA_EMB_LNB", "1") != "0"
 # the FFN's dz chained into its consumer's sca_gemm_lnb launch: parity-green, but -1.7 % in
 # step at config 2 (three 256-column passes at one workgroup per CU lose to the stand-alone
 # NN GEMM that shares the CUs with the weight gradients; tools/ab_dz.sh) — off by default
@@ -398,7 +401,8 @@ def gemm_lnb(probs, lnp):
     larr = (L.GemmLnbProblem * len(lnp))(*[L.GemmLnbProblem(o.v.data_ptr(), o.mean.data_ptr(), o.rstd.data_ptr(),
                                                            o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr(),
                                                            ptr(o.wo) if chain else None, ptr(dout[g]),
-                                                           ptr(o.aux) if chain else None, n2 // 256, n2)
+                                                           ptr(o.aux) if chain else None, n2 // 256, n2,
+                                                           ptr(o.tab), o.T)
                                             for g, o in enumerate(lnp)])
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
@@ -1263,6 +1267,13 @@ class LayerNormAdd(Function):
         ctx.G, ctx.pos, ctx.has_post, ctx.act, ctx.r_mod, ctx.r_off = G, pos_table, has_post, act, r_mod, r_off
         ctx.drop_p, ctx.seeds = drop_p, seeds
         ctx.bet = tuple(bet)  # parameters (leaves): identify their gradients' slots
+        # the embedding LayerNorm (position table, no tail, no dropout): its backward can ride
+        # in the consuming attention block's input-gradient GEMM (sca_gemm_lnb, tab mode)
+        ctx.lnsaved = None
+        if pos_table and not has_post and not act and drop_p == 0 and N == 256 and _FUSE_LNB and _EMB_LNB:
+            ctx.lnsaved = [LnSaved(x[g], means[g], rstds[g], gam[g], tab=tab[g], T=T) for g in range(G)]
+            for y, o in zip(ys, ctx.lnsaved):
+                y._sca_ln = o
         ctx.save_for_backward(*x, *(tab if pos_table else []), *gam, *means, *rstds, *(ys if act else []))
         return tuple(ys)
 
@@ -1283,21 +1294,29 @@ class LayerNormAdd(Function):
             dys = dd
         N = x[0].shape[-1]
         rows = x[0].numel() // N
-        nblk = L.lib().sca_layernorm_bwd_blocks(rows)
-        dx = [torch.empty_like(t) for t in x]
+        hs = _take_handoff(ctx.lnsaved, dys)  # the consumer's sca_gemm_lnb ran this backward
+        ctx.lnsaved = None
         dpost = [torch.empty_like(t) for t in x] if ctx.has_post else [None] * G
         dg = [param_grad_empty(t) for t in gam]
         db = [param_grad_empty(t) for t in ctx.bet]
-        part = [x[0].new_empty(2 * nblk * N) for _ in range(G)]
-        for c in range(0, G, L.LN_MAX_PROBLEMS):
-            gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
-            arr = (L.LnBwdProblem * len(gs))(*[L.LnBwdProblem(dys[g].data_ptr(), x[g].data_ptr(), ptr(tab[g]),
-                                                                gam[g].data_ptr(), means[g].data_ptr(),
-                                                                rstds[g].data_ptr(), ptr(ys[g]), act,
-                                                                ptr(dpost[g]), dx[g].data_ptr(), dg[g].data_ptr(),
-                                                                db[g].data_ptr(), part[g].data_ptr()) for g in gs])
-            L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, ctx.r_mod, ctx.r_off, 0, L.stream_handle()),
-                    "sca_layernorm_bwd")
+        if hs is not None:  # dL/dv (= dL/dx) done; the dgamma / dbeta partials summed here
+            dx, part, nblk = [h[2] for h in hs], [h[3] for h in hs], hs[0][4]
+            reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
+                        [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0)
+        else:
+            nblk = L.lib().sca_layernorm_bwd_blocks(rows)
+            dx = [torch.empty_like(t) for t in x]
+            part = [x[0].new_empty(2 * nblk * N) for _ in range(G)]
+            for c in range(0, G, L.LN_MAX_PROBLEMS):
+                gs = range(c, min(G, c + L.LN_MAX_PROBLEMS))
+                arr = (L.LnBwdProblem * len(gs))(*[L.LnBwdProblem(dys[g].data_ptr(), x[g].data_ptr(), ptr(tab[g]),
+                                                                    gam[g].data_ptr(), means[g].data_ptr(),
+                                                                    rstds[g].data_ptr(), ptr(ys[g]), act,
+                                                                    ptr(dpost[g]), dx[g].data_ptr(),
+                                                                    dg[g].data_ptr(), db[g].data_ptr(),
+                                                                    part[g].data_ptr()) for g in gs])
+                L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, ctx.r_mod, ctx.r_off, 0,
+                                                  L.stream_handle()), "sca_layernorm_bwd")
         params_produced(list(gam) + list(ctx.bet))
         dtab = []
         if pos:
