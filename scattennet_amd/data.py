@@ -158,8 +158,15 @@ def prepare_batch(samples, cfg, split, joint_parts=None, device="cuda"):
     train = split == "train"
     min_rate, max_rate = (0.5, 1.5) if train else (1.0, 1.0)
     picks, ops, affs, raws = [], [], [], []
+    if not samples:
+        raise ValueError("prepare_batch: empty batch")
     for kp in samples:
         kp = np.asarray(kp)
+        # the kernel reads 2 * K_all floats per frame: a (T, K, 4) array that skipped
+        # load_sample's [:, :, :-2] trim, or clips of different K_all, would be read at the
+        # wrong stride
+        if kp.ndim != 3 or kp.shape[-1] != 2 or kp.shape[1] != np.shape(samples[0])[1]:
+            raise ValueError(f"prepare_batch: every sample must be (T, K_all, 2) with one K_all; got {kp.shape}")
         picks.append(select_frames(kp.shape[0], train, cfg["max_len"], min_rate, max_rate))
         ops.append(augmentation_draw(train))
         affs.append(augmentation_affine(ops[-1]))

@@ -3,9 +3,7 @@
 Runs ONLY in the build container, where `/root/reference` is importable: the reference's
 augmentation.py (numpy only: rotate_keypoints, flip_keypoints) is imported and applied to a
 fixed keypoint array; writes `augment.npz` (data only) and its entry in `manifest.json`.
-(dataset.py itself — frame selection, normalisation — cannot be imported here: it imports
-the reference's utils.py, which needs loguru; those stay "parity unpinned", tests/
-test_data_normalize.py.)
+(dataset.py's selection / normalisation / collator vectors: gen_golden_dataset.py.)
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden_augment.py
 """

@@ -1,11 +1,11 @@
 """Input contract: SLR_Dataset.normalize_keypoints and the keypoint
 fields of its collator (dataset.py:58-170).
 
-PARITY UNPINNED by the reference itself: dataset.py imports the reference's utils.py, which
-needs loguru (absent in this image), so the module cannot be imported to capture vectors.
-The oracle restatement (oracle/sca_oracle.py:normalize_keypoints) is checked here against an
-independent scalar restatement written straight from dataset.py:141-170 and hand-computed
-cases; the HIP kernel (sca_normalize_parts) is checked against the oracle on the GPU.
+The oracle restatement (oracle/sca_oracle.py:normalize_keypoints) is pinned to the
+reference's own dataset.py in tests/test_dataset_golden.py; here it is also checked against
+an independent scalar restatement written straight from dataset.py:141-170 and hand-computed
+cases, and the HIP kernel (sca_normalize_parts) against the oracle on the GPU (overlapping
+parts, several joint layouts).
 """
 import numpy as np
 import pytest

@@ -5,10 +5,10 @@ the on-disk sample format (dataset.py:40-56), frame selection (:185-215), augmen
 * augmentation: the oracle's rotate / flip are pinned to vectors produced by the
   reference's own augmentation.py (tests/golden/gen_golden_augment.py); the composed
   per-clip affine the kernel applies is checked against them;
-* frame selection and the augmentation draw: PARITY UNPINNED by the reference (dataset.py
-  cannot be imported here: its utils.py needs loguru) — checked against a scalar
-  restatement of the reference's RNG call sequence written straight from dataset.py
-  (same seeds -> same draws), and for the properties the reference asserts;
+* frame selection and the augmentation draw: pinned to the reference's own dataset.py in
+  tests/test_dataset_golden.py (seeded select_frames sequences, whole collator batches);
+  here also against a scalar restatement of the reference's RNG call sequence (same seeds
+  -> same draws), and for the properties the reference asserts;
 * the GPU launch (sca_prepare_keypoints): against the oracle pipeline (oracle.prepare_sample)
   with the same decisions, fp32 (the reference rotates in float64: rounding-level
   differences, bound 1e-5 absolute on [0, 1] coordinates).
@@ -123,6 +123,17 @@ def test_selection_properties():
         lo, hi = min(int(0.5 * n), 256), min(int(1.5 * n), 256)
         assert lo <= len(idx) <= hi + 1  # random.randint(lo, hi + 1), inclusive (0 frames possible at n = 1)
         assert len(idx) == 0 or (idx.min() >= 0 and idx.max() < n)
+
+
+def test_prepare_batch_rejects_bad_sample_shapes():
+    from scattennet_amd import data as D
+    cfg = {"max_len": 16, "normalize": False, "joint_parts": PARTS}
+    bad = [[np.zeros((5, 75, 4), np.float32)],  # load_sample's [:, :, :-2] trim skipped
+           [np.zeros((5, 75, 2), np.float32), np.zeros((5, 74, 2), np.float32)],  # mixed K_all
+           [np.zeros((75, 2), np.float32)], []]
+    for samples in bad:
+        with pytest.raises(ValueError):
+            D.prepare_batch(samples, cfg, "dev", device="cpu")
 
 
 def test_load_sample_format(tmp_path):
