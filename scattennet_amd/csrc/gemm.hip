@@ -59,7 +59,10 @@ struct Operand {
 
 // Load one BK-slice of an operand tile from global into registers (zero outside bounds).
 // KCONTIG: global element (row, k) at base[row * ld + k];  else at base[k * ld + row].
-template <bool KCONTIG, int ROWS, int BK, int NT>
+// VEC = false: element-wise loads with every element bounds-checked — the any-shape path
+// (K, ld not multiples of 4, operands not 16-byte aligned: CoordinatesFusion's per-clip
+// (T/4 x T/4) attention at any frame count, model/fusion.py:52-55).
+template <bool KCONTIG, int ROWS, int BK, int NT, bool VEC = true>
 __device__ __forceinline__ void load_tile(f32x4* reg, const float* base, int ld, int row0, int nrows, int k0,
                                           int kend) {
 #pragma unroll
@@ -75,7 +78,16 @@ __device__ __forceinline__ void load_tile(f32x4* reg, const float* base, int ld,
     }
     const int gr = row0 + row, gk = k0 + k;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (KCONTIG) {
+    if (!VEC) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (KCONTIG) {
+          if (gr < nrows && gk + j < kend) v[j] = base[(long)gr * ld + gk + j];
+        } else if (gk < kend && gr + j < nrows) {
+          v[j] = base[(long)gk * ld + gr + j];
+        }
+      }
+    } else if (KCONTIG) {
       if (gr < nrows && gk < kend) v = ld4(base + (long)gr * ld + gk);
     } else if (gk < kend) {
       if (gr + 3 < nrows) {
@@ -246,7 +258,7 @@ __device__ __forceinline__ void slab_rows(float* slab, const f32x4 (&v)[4], int 
   }
 }
 
-template <int LAYOUT, class C>
+template <int LAYOUT, class C, bool VEC = true>
 __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NT = C::NT, RM = C::RM, RN = C::RN;
   constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
@@ -314,8 +326,8 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
     while (s + 1 < P.nseg && t >= seg_n[s]) { t -= seg_n[s]; ++s; }
     const sca_gemm_seg& S = P.seg[s];
     const int k0 = seg_kbeg[s] + t * BK;
-    load_tile<A_KC, BM, BK, NT>(ra, S.A, S.lda, m0, P.M, k0, seg_kend[s]);
-    load_tile<B_KC, BN, BK, NT>(rb, S.B, S.ldb, n0, P.N, k0, seg_kend[s]);
+    load_tile<A_KC, BM, BK, NT, VEC>(ra, S.A, S.lda, m0, P.M, k0, seg_kend[s]);
+    load_tile<B_KC, BN, BK, NT, VEC>(rb, S.B, S.ldb, n0, P.N, k0, seg_kend[s]);
     alpha_f = S.alpha;
   };
   auto compute = [&](const float* As, const float* Bs) {
@@ -1689,10 +1701,10 @@ int launch_persistent(GemmArgs& a, int nprob, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-template <int LAYOUT, class C>
+template <int LAYOUT, class C, bool VEC = true>
 int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + C::BN - 1) / C::BN, (maxM + C::BM - 1) / C::BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_kernel<LAYOUT, C>), grid, dim3(C::NT), 0, st, a);
+  hipLaunchKernelGGL((gemm_kernel<LAYOUT, C, VEC>), grid, dim3(C::NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -1744,8 +1756,23 @@ int launch_glds2(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t s
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
+// float4 operand loads need K (k-contiguous operands), lda, ldb multiples of 4 and A, B
+// 16-byte aligned; otherwise the element-wise (any-shape) form of the register-staged kernel
+bool vec_ok(const GemmArgs& a, int nprob, int layout) {
+  const bool a_kc = layout != SCA_GEMM_TN, b_kc = layout == SCA_GEMM_NT;
+  for (int i = 0; i < nprob; ++i)
+    for (int s = 0; s < a.p[i].nseg; ++s) {
+      const sca_gemm_seg& S = a.p[i].seg[s];
+      if (((a_kc || b_kc) && (S.K & 3)) || (S.lda & 3) || (S.ldb & 3) ||
+          (reinterpret_cast<uintptr_t>(S.A) & 15) || (reinterpret_cast<uintptr_t>(S.B) & 15))
+        return false;
+    }
+  return true;
+}
+
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
   if (tile > 10 && tile < 20 && !persistent_ok(a, nprob)) tile = 1;
   if (tile >= 20 && !glds_ok(a, nprob)) tile = LAYOUT == SCA_GEMM_TN ? 5 : (LAYOUT == SCA_GEMM_NN ? 7 : 1);
   switch (tile) {
@@ -1829,11 +1856,10 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
     for (int s = 0; s < P.nseg; ++s) {
       const sca_gemm_seg& S = P.seg[s];
       const bool a_kc = layout != SCA_GEMM_TN, b_kc = layout == SCA_GEMM_NT;
-      // K must be a multiple of 4 when an operand is k-contiguous (float4 loads along k); the
-      // TN layout (weight gradients: K = B*T rows) takes any K
-      if (((a_kc || b_kc) && (S.K & 3)) || !S.A || !S.B || (S.lda & 3) || (S.ldb & 3) ||
-          (reinterpret_cast<uintptr_t>(S.A) & 15) || (reinterpret_cast<uintptr_t>(S.B) & 15)) {
-        sca_set_error("sca_gemm: K (NT/NN), lda, ldb must be multiples of 4 and A/B 16-byte aligned");
+      // any K, lda, ldb and operand alignment: shapes the float4 loads cannot take run the
+      // element-wise form of the register-staged kernel (vec_ok)
+      if (!S.A || !S.B || S.K < 0 || (reinterpret_cast<uintptr_t>(S.A) & 3) || (reinterpret_cast<uintptr_t>(S.B) & 3)) {
+        sca_set_error("sca_gemm: null or misaligned (not 4-byte) operand, or negative K");
         return SCA_ERR_ARG;
       }
       if ((a_kc && S.lda < S.K) || (!a_kc && S.lda < P.M) || (b_kc && S.ldb < S.K) || (!b_kc && S.ldb < P.N)) {
@@ -1875,7 +1901,8 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
   const int tile = pick_tile(layout, tiles64, splitk);
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
-  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22) && glds_ok(a, nprob)) {
+  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22) && glds_ok(a, nprob) &&
+      vec_ok(a, nprob, layout)) {
     a.counters = counters;
     do_reduce = false;
   }

@@ -43,9 +43,29 @@ WORKLOADS = {
     "cfg3": dict(B=8, T=256, K_all=542, groups=[6, 21, 21], d=256, H=16, L=4, residual=True, maxpos=256,
                  fusion=True, joint_idx=[list(range(11, 17)), list(range(33, 54)), list(range(54, 75))],
                  residual_blocks=[256, 256, 512, 512], in_fusion=512, out_fusion=1024),
+    # config 3 at a padded batch length that is not a multiple of 16 (the collator pads to the
+    # longest clip, dataset.py:76-89): two pools leave 58 frames for the fusion (parity case)
+    "cfg3_t234": dict(B=4, T=234, K_all=542, groups=[6, 21, 21], d=256, H=16, L=4, residual=True, maxpos=256,
+                      fusion=True, joint_idx=[list(range(11, 17)), list(range(33, 54)), list(range(54, 75))],
+                      residual_blocks=[256, 256, 512, 512], in_fusion=512, out_fusion=1024),
+    # the Phoenix-2014 yaml model section (configs/phoenix-2014.yaml:211-220): residual
+    # [256, 256] (one pool), fusion 256 -> 1024; odd T = 181 -> 90 frames (parity case)
+    "cfg2014_t181": dict(B=4, T=181, K_all=542, groups=[6, 21, 21], d=256, H=16, L=4, residual=True, maxpos=256,
+                         fusion=True, joint_idx=[list(range(11, 17)), list(range(33, 54)), list(range(54, 75))],
+                         residual_blocks=[256, 256], in_fusion=256, out_fusion=1024),
     # BASELINE config 5: long sequence, 133 joints split COCO-WholeBody style
     "cfg5": dict(B=8, T=1024, K_all=133, groups=[23, 68, 21, 21], d=512, H=16, L=4, residual=False, maxpos=1024),
 }
+
+
+def pooled_frames(w):
+    """Frames after the residual network: MaxPool1d(2, 2) (floor) on every even-indexed block
+    (model/residual.py:22-23, 40-43)."""
+    t = w["T"]
+    for i in range(len(w.get("residual_blocks", [w["d"], w["d"], 2 * w["d"], 2 * w["d"]]))):
+        if i % 2 == 0:
+            t //= 2
+    return t
 
 
 def encoder_cfg(w):
@@ -123,7 +143,7 @@ def synthetic_batch(w, device, seed=0, ragged=False):
         for b, n in enumerate(lens):
             mask[b, n:] = 0
     if w.get("fusion"):
-        gout = torch.randn(1, B, T // 4, w["out_fusion"], generator=torch.Generator().manual_seed(1))
+        gout = torch.randn(1, B, pooled_frames(w), w["out_fusion"], generator=torch.Generator().manual_seed(1))
     else:
         gout = torch.randn(len(w["groups"]), B, T, w["d"], generator=torch.Generator().manual_seed(1))
     return kp.to(device), mask.to(device), gout.to(device)
@@ -148,7 +168,8 @@ def flops_per_step(w):
                     rows //= 2
         total += 3 * f
     if w.get("fusion"):
-        n4, t4, ci, co = N // 4, T // 4, w["in_fusion"], w["out_fusion"]
+        t4 = pooled_frames(w)
+        n4, ci, co = B * t4, w["in_fusion"], w["out_fusion"]
         f = 3 * 2 * n4 * ci * co + 2 * 2 * B * t4 * t4 * co + 2 * n4 * co * co * 2 + 2 * 2 * n4 * co * 3 * co
         total += 3 * f
     return total

@@ -137,3 +137,53 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
         ops.set_grad_sink(None)
         if init_here:
             dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
+    """BASELINE config 4's shape in one process: the config-3 encoder (3 streams + residual +
+    fusion) at B = 64 = 8 shards x 8 clips.  The eight shards' HIP gradients summed equal
+    the full 64-clip HIP gradient and the (tie-aware) oracle's full-batch gradient, within
+    the north-star 1e-3 — what the 8-GPU all-reduce of config 4 computes."""
+    from scattennet_amd import workloads as W
+    from tests.test_gpu_scale import hip_encoder_step, tie_aware_encoder_oracle
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    w = dict(W.WORKLOADS["cfg3"], B=64)
+    enc = W.build_encoder(w, dev, seed=8, init="random").eval()
+    kp, mask, gout = W.synthetic_batch(w, dev, seed=12, ragged=False)
+    g = torch.Generator().manual_seed(22)
+    lens = torch.randint(1, w["T"] + 1, (64,), generator=g)
+    lens[5], lens[40], lens[63] = w["T"], 1, 0
+    mask = (torch.arange(w["T"])[None] < lens[:, None]).long().to(dev)
+    named = dict(enc.named_parameters())
+    for p in enc.parameters():
+        p.grad = None
+    fuse, pool_inputs, relu_outputs = hip_encoder_step(enc, kp, mask, gout[0], monkeypatch)
+    full = {k: p.grad.detach().clone() for k, p in named.items() if p.grad is not None}
+    shard_sum = {}
+    for s in range(8):
+        for p in enc.parameters():
+            p.grad = None
+        sl = slice(8 * s, 8 * s + 8)
+        out = enc(kp[sl], mask[sl])[0]
+        out.backward(gout[0, sl].contiguous())
+        torch.cuda.synchronize()
+        # per-clip forward of the shard = the full batch's rows (tile shapes may differ with M:
+        # summation order only)
+        assert rel_err(out, fuse[sl]) < 1e-5, s
+        for k, p in named.items():
+            if p.grad is not None:
+                shard_sum[k] = shard_sum[k] + p.grad if k in shard_sum else p.grad.detach().clone()
+    assert set(full) == set(shard_sum)
+    gscale = max(float(v.abs().max()) for v in full.values())
+    for k in full:
+        assert close(shard_sum[k].cpu(), full[k].cpu(), PARITY_TOL, gscale), (k, rel_err(shard_sum[k], full[k]))
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref, grads, stats = tie_aware_encoder_oracle(enc, w, kp, mask, gout[0], pool_inputs, relu_outputs, monkeypatch)
+    print("cfg4 shape (cfg3 at B = 64) ties:", stats)
+    assert rel_err(fuse, ref) < PARITY_TOL
+    rscale = max(float(v.abs().max()) for v in grads.values())
+    for k, v in grads.items():
+        assert close(shard_sum[k].cpu(), v, PARITY_TOL, rscale), (k, rel_err(shard_sum[k].cpu(), v))

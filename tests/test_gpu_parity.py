@@ -122,7 +122,7 @@ def test_coordinate_mapping():
     _check(fx, m, out, i, ("x_coord", "y_coord"))
 
 
-@pytest.mark.parametrize("name", ["residual_64_64_128_128", "residual_64_64"])
+@pytest.mark.parametrize("name", ["residual_64_64_128_128", "residual_64_64", "residual_64_64_T45"])
 def test_residual_network(name):
     import scattennet_amd as S
     dev = _dev()
@@ -142,11 +142,50 @@ def test_keypoint_module():
     _check(fx, m, m(i["keypoints"], i["mask"]), i, ("keypoints",))
 
 
-def test_coordinates_fusion():
+# T/4 = 16, and frame counts whose per-clip (T/4 x T/4) attention has rows that are not a
+# multiple of 4 floats (the any-shape GEMM form): the reference's own smoke size 45, odd 13
+@pytest.mark.parametrize("name", ["fusion", "fusion_T45", "fusion_T13"])
+def test_coordinates_fusion(name):
     import scattennet_amd as S
     dev = _dev()
-    fx = load("fusion")
+    fx = load(name)
     m = _load(S.CoordinatesFusion(fx["meta"]["in"], fx["meta"]["out"], 0.2), fx, dev)
     gi = ("left", "right", "body")
     i = _inputs(fx, dev, gi)
     _check(fx, m, m(i["left"], i["right"], i["body"]), i, gi)
+
+
+def test_xstream_cfg1():
+    """BASELINE config 1 (B=2 T=64 K=27 d=64 H=4, x-stream, L = 2 as captured) through the
+    HIP drop-ins: CoordinateMapping's x half (model/layers.py:111-123), the self position
+    embedding + first LayerNorm (keypoint_module.py:155, 161, one fused launch) and the self
+    layers (:176-178) — against the reference's own vectors (gen_golden_xstream.py)."""
+    import scattennet_amd as S
+    from scattennet_amd.layers import coordinate_mapping_grouped, pos_embed_layernorm_grouped
+    from torch import nn
+    dev = _dev()
+    fx = load("xstream_cfg1")
+    cfg, K = fx["meta"]["cfg"], fx["meta"]["K"]
+
+    class XStream(nn.Module):  # the fixture's module tree (KeypointModule key names)
+        def __init__(self):
+            super().__init__()
+            self.coordinate_mapping = S.CoordinateMapping(K, cfg["d_model"])
+            self.sca = nn.Module()
+            self.sca.self_attn_layers = nn.ModuleList([S.CoordinateAttention(cfg, "self_attn")
+                                                       for _ in range(cfg["attn_layers"])])
+            self.sca.first_self_norm = nn.LayerNorm(cfg["d_model"])
+            self.sca.self_pos_embed = S.LearningPositionEmbedding(cfg["max_position_embeddings"], cfg["d_model"])
+
+        def forward(self, keypoints, mask):
+            cm = self.coordinate_mapping
+            xe, _ = coordinate_mapping_grouped([cm], keypoints, [cm.joint_index(keypoints.device)])
+            s = pos_embed_layernorm_grouped([self.sca.self_pos_embed], [self.sca.first_self_norm], xe)[0]
+            m = S.create_attention_mask(mask, s.dtype)
+            for layer in self.sca.self_attn_layers:
+                s = layer(s, m)
+            return s
+
+    m = _load(XStream(), fx, dev)
+    i = _inputs(fx, dev, ("keypoints",))
+    _check(fx, m, m(i["keypoints"], i["mask"]), i, ("keypoints",))

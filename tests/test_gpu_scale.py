@@ -113,27 +113,10 @@ def _tie_aware_relu(z, gpu_out, stats):
     return torch.where(torch.where(tie, theirs, mine), z, torch.zeros_like(z))
 
 
-def test_cfg3_full_encoder_vs_oracle(monkeypatch):
-    """BASELINE config 3: yaml model section, 3 streams + residual + fusion, ragged masks;
-    output and EVERY gradient at the north-star 1e-3.
-
-    ReLU + MaxPool1d(2,2) make the gradient discontinuous at ReLU inputs that are zero, and at
-    pool pairs whose two values are equal, to within fp32 forward rounding (at this seed e.g.
-    right_encoder.residual.blocks.2 has pairs 4e-6 apart at magnitude 6): which element
-    receives the gradient there is decided by rounding in either implementation.  The oracle
-    therefore pools such pairs and passes such ReLU inputs — those closer (to each other / to
-    zero) than twice the two implementations' measured deviation on that tensor, which is
-    itself checked to be below 1e-4 of its scale; detected and counted — the way the GPU
-    did, from the GPU's own pool inputs / ReLU outputs; outside them the two decisions must
-    agree.  No gradient tolerance is relaxed."""
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
+def hip_encoder_step(enc, kp, mask, gout, monkeypatch):
+    """Forward + backward of the HIP encoder, recording the GPU's max-pool inputs and ReLU
+    outputs per block (for the tie-aware oracle below).  -> (fuse, pool_inputs, relu_outputs)."""
     from scattennet_amd import ops
-    torch.set_num_threads(min(16, torch.get_num_threads()))
-    dev = torch.device("cuda:0")
-    w = W.WORKLOADS["cfg3"]
-    enc = W.build_encoder(w, dev, seed=4, init="random").eval()  # parity at eval (dropout off)
-    kp, mask, gout = W.synthetic_batch(w, dev, seed=6, ragged=True)
     pool_inputs = []  # per downsampling block: [body, left, right] (the grouped launch order)
     relu_outputs = []  # per residual block: norm1 -> ReLU, then norm2 + shortcut -> ReLU
     fwd, lnfwd = ops.MaxPoolT.forward, ops.LayerNormAdd.forward
@@ -150,15 +133,24 @@ def test_cfg3_full_encoder_vs_oracle(monkeypatch):
 
     monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(recording))
     monkeypatch.setattr(ops.LayerNormAdd, "forward", staticmethod(ln_recording))
-    fuse = enc(kp, mask)[0]
-    fuse.backward(gout[0])
-    torch.cuda.synchronize()
-    monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(fwd))
-    monkeypatch.setattr(ops.LayerNormAdd, "forward", staticmethod(lnfwd))
-    assert len(pool_inputs) == 2 and all(len(c) == 3 for c in pool_inputs)
+    try:
+        fuse = enc(kp, mask)[0]
+        fuse.backward(gout)
+        torch.cuda.synchronize()
+    finally:
+        monkeypatch.setattr(ops.MaxPoolT, "forward", staticmethod(fwd))
+        monkeypatch.setattr(ops.LayerNormAdd, "forward", staticmethod(lnfwd))
+    return fuse, pool_inputs, relu_outputs
 
+
+def tie_aware_encoder_oracle(enc, w, kp, mask, gout, pool_inputs, relu_outputs, monkeypatch):
+    """The oracle encoder (fwd + bwd, CPU) resolving the rounding-level max-pool / ReLU ties
+    the way the GPU did (from its recorded pool inputs / ReLU outputs), checking that every
+    other decision agrees.  -> (fuse, {param: grad}, stats)."""
     cfg = W.encoder_cfg(w)
     nblk = len(cfg["residual_blocks"])
+    npool = (nblk + 1) // 2
+    assert len(pool_inputs) == npool and all(len(c) == 3 for c in pool_inputs)
     assert len(relu_outputs) == 2 * nblk and all(len(c) == 3 for c in relu_outputs)
     order = iter([(s, i) for s in range(3) for i in range(nblk)])  # oracle: body, left, right
     stats = {"ties": 0, "flipped": 0, "disagree_outside_ties": 0,
@@ -173,10 +165,43 @@ def test_cfg3_full_encoder_vs_oracle(monkeypatch):
                             relu_outputs[2 * i + 1][s], stats)
         return _tie_aware_pool(o, pool_inputs[i // 2][s], stats) if downsample else o
 
+    orig = O.residual_block
     monkeypatch.setattr(O, "residual_block", residual_block)
-    ref, grads = _encoder_oracle(enc, cfg, kp.cpu(), mask.cpu(), gout[0].cpu())
-    print(f"cfg3 max-pool pairs / ReLU inputs: {stats}")
+    try:
+        ref, grads = _encoder_oracle(enc, cfg, kp.cpu(), mask.cpu(), gout.cpu())
+    finally:
+        monkeypatch.setattr(O, "residual_block", orig)
     assert stats["disagree_outside_ties"] == 0 and stats["relu_disagree_outside_ties"] == 0, stats
+    return ref, grads, stats
+
+
+@pytest.mark.parametrize("wname", ["cfg3", "cfg3_t234", "cfg2014_t181"])
+def test_full_encoder_vs_oracle(monkeypatch, wname):
+    """BASELINE config 3: yaml model section, 3 streams + residual + fusion, ragged masks;
+    output and EVERY gradient at the north-star 1e-3.  Also at frame counts a real padded
+    batch has (dataset.py:76-89): T = 234 (58 frames reach the fusion) and the 2014 yaml
+    (residual [256, 256], one pool, fusion 256 -> 1024) at odd T = 181 (90 frames).
+
+    ReLU + MaxPool1d(2,2) make the gradient discontinuous at ReLU inputs that are zero, and at
+    pool pairs whose two values are equal, to within fp32 forward rounding (at this seed e.g.
+    right_encoder.residual.blocks.2 has pairs 4e-6 apart at magnitude 6): which element
+    receives the gradient there is decided by rounding in either implementation.  The oracle
+    therefore pools such pairs and passes such ReLU inputs — those closer (to each other / to
+    zero) than twice the two implementations' measured deviation on that tensor, which is
+    itself checked to be below 1e-4 of its scale; detected and counted — the way the GPU
+    did, from the GPU's own pool inputs / ReLU outputs; outside them the two decisions must
+    agree.  No gradient tolerance is relaxed."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    dev = torch.device("cuda:0")
+    w = W.WORKLOADS[wname]
+    enc = W.build_encoder(w, dev, seed=4, init="random").eval()  # parity at eval (dropout off)
+    kp, mask, gout = W.synthetic_batch(w, dev, seed=6, ragged=True)
+    fuse, pool_inputs, relu_outputs = hip_encoder_step(enc, kp, mask, gout[0], monkeypatch)
+    assert fuse.shape[1] == W.pooled_frames(w)
+    ref, grads, stats = tie_aware_encoder_oracle(enc, w, kp, mask, gout[0], pool_inputs, relu_outputs, monkeypatch)
+    print(f"{wname} max-pool pairs / ReLU inputs: {stats}")
     assert rel_err(fuse, ref) < PARITY_TOL
     gscale = max(float(t.abs().max()) for t in grads.values())
     named = dict(enc.named_parameters())
@@ -188,7 +213,7 @@ def test_cfg3_full_encoder_vs_oracle(monkeypatch):
             bad.append(k)
         if float(gr.abs().max()) >= 1e-4 * gscale:  # (not an analytically-zero gradient)
             errs.append((round(rel_err(got, gr), 6), k))
-    print("cfg3 largest gradient errors:", sorted(errs, reverse=True)[:6])
+    print(f"{wname} largest gradient errors:", sorted(errs, reverse=True)[:6])
     assert not bad, bad
     for k, prm in named.items():  # parameters the reference never trains (long shortcuts)
         if k not in grads:

@@ -89,13 +89,14 @@ def test_keypoint_module():
          ("keypoints",))
 
 
-@pytest.mark.parametrize("name", ["residual_64_64_128_128", "residual_64_64"])
+@pytest.mark.parametrize("name", ["residual_64_64_128_128", "residual_64_64", "residual_64_64_T45"])
 def test_residual_network(name):
     _run(name, lambda p, i, m: O.residual_network(p, "", i["x"], m["blocks"]), ("x",))
 
 
-def test_fusion():
-    _run("fusion", lambda p, i, m: O.coordinates_fusion(p, "", i["left"], i["right"], i["body"]),
+@pytest.mark.parametrize("name", ["fusion", "fusion_T45", "fusion_T13"])
+def test_fusion(name):
+    _run(name, lambda p, i, m: O.coordinates_fusion(p, "", i["left"], i["right"], i["body"]),
          ("left", "right", "body"))
 
 
