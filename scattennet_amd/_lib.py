@@ -213,3 +213,20 @@ def require_device(*tensors):
         if t is not None and (not t.is_cuda or t.dtype != torch.float32):
             raise RuntimeError("scattennet_amd ops run only on ROCm (MI355X) fp32 tensors; got "
                                f"{t.device} {t.dtype}.  There is no CPU fallback.")
+
+
+def source_digest():
+    """sha256 (first 16 hex digits) of the HIP library's sources (csrc/*.hip, *.h, *.cpp and
+    include/scatten.h): identifies the build a committed rocprofv3 profile was measured on
+    (bench.py reports the profile's figures only for a matching build)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.dirname(_HERE)
+    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h")) +
+                   glob.glob(os.path.join(_HERE, "csrc", "*.cpp")) + [os.path.join(root, "include", "scatten.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]

@@ -175,23 +175,27 @@ def dropout_grouped(xs, p):
 
 # split-K slabs combined inside the GEMM launch by the last-arriving split (sca_gemm_splitk_fused)
 _SPLITK_FUSED = __import__("os").environ.get("SCA_SPLITK_FUSED", "1") != "0"
-_CNT = None
-_CNT_POS = 0
+_CNT = {}  # device index -> [ring, position]
 _CNT_SIZE = 1 << 16
 
 
-def _splitk_counters(n):
-    """n zeroed tile counters from a persistent ring (the kernel leaves them zero); launches
-    far enough apart to share a slot have long completed (a step uses < 32k)."""
-    global _CNT, _CNT_POS
-    if _CNT is None:
-        _CNT = torch.zeros(_CNT_SIZE, dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+def _splitk_counters(n, device=None):
+    """n zeroed tile counters from a persistent per-device ring (the kernel leaves them
+    zero).  A slot is reused only after the whole ring (65,536 counters) has been handed out
+    since; one config-2 step uses ~6k, so the launches that shared a slot have completed
+    (every launch of a step is ordered before the next step's)."""
+    dev = torch.cuda.current_device() if device is None else device
+    if n > _CNT_SIZE:
+        raise RuntimeError(f"split-K launch needs {n} tile counters, more than the ring's {_CNT_SIZE}")
+    ent = _CNT.get(dev)
+    if ent is None:
+        ent = _CNT[dev] = [torch.zeros(_CNT_SIZE, dtype=torch.int32, device=torch.device("cuda", dev)), 0]
+    ring, pos = ent
     n = -(-n // 64) * 64
-    if _CNT_POS + n > _CNT_SIZE:
-        _CNT_POS = 0
-    t = _CNT[_CNT_POS:_CNT_POS + n]
-    _CNT_POS += n
-    return t
+    if pos + n > _CNT_SIZE:
+        pos = 0
+    ent[1] = pos + n
+    return ring[pos:pos + n]
 
 
 def gemm(layout, probs, splitk=1, ws=None):
@@ -203,7 +207,8 @@ def gemm(layout, probs, splitk=1, ws=None):
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
         if splitk > 1 and _SPLITK_FUSED and "sca_gemm_splitk_fused" not in L.MISSING:
             cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
-                                                                max(p.N for p in chunk)))
+                                                                max(p.N for p in chunk)),
+                                   ws.device.index if ws is not None else None)
             with _timed(_GEMM_NAMES[layout], flops):
                 L.check(lib.sca_gemm_splitk_fused(layout, len(chunk), arr, splitk, ptr(ws), ptr(cnt), st),
                         "sca_gemm_splitk_fused")

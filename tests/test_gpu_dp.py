@@ -73,6 +73,14 @@ def test_half_batch_gradients_sum_to_full_batch():
 
 @pytest.mark.gpu
 def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
+    """At world size 1 the all-reduce is an identity and the 1/world pre-scale is x1, so a
+    missing or late wait of the communication stream on a producing stream would go unseen:
+    the collective is wrapped so that it DOUBLES its bucket on the communication stream
+    before reducing it — every gradient must then come out exactly 2x the plain HIP one, in
+    the eager step and in the graph replay (a bucket reduced before its last gradient
+    landed would not be doubled)."""
+    import warnings
+
     import torch.distributed as dist
 
     from scattennet_amd import ops, workloads as W
@@ -91,6 +99,13 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
         port = 29400 + os.getpid() % 500
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                 device_id=dev)
+    real_all_reduce = dist.all_reduce
+
+    def doubling_all_reduce(t, *a, **k):  # on the stream the reducer issues from
+        t.mul_(2.0)
+        return real_all_reduce(t, *a, **k)
+
+    monkeypatch.setattr(dist, "all_reduce", doubling_all_reduce)
     red = GradBuckets(model.parameters(), bucket_mb=6)
     try:
         assert red.collective and red.overlap
@@ -109,13 +124,18 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
         eager = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
         for p in params:
             p.grad = None
+        # drop the eager step's autograd graph: its AccumulateGrad nodes (bound to stream s)
+        # would otherwise be reused by the captured backward — an unrecorded fork into s
+        del outs
         red.quiesce()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # RCCL watchdog thread
-            led = ops.fork_ledger_begin()
-            outs = model(kp, mask)
-            torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
-            ops.fork_ledger_end()  # every fork (side streams, branch, RCCL) joined into the origin
+        with warnings.catch_warnings():
+            warnings.filterwarnings("error", message=".*AccumulateGrad.*")
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # RCCL watchdog thread
+                led = ops.fork_ledger_begin()
+                outs = model(kp, mask)
+                torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+                ops.fork_ledger_end()  # every fork (side streams, branch, RCCL) joined into the origin
         assert led.last_fork and any("RCCL" in n for n in led.names.values())
         for p in params:  # poison the buckets: the replay must rewrite every planned gradient
             if p.grad is not None:
@@ -129,8 +149,8 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
         assert all(0 <= v < red.flat.numel() * 4 for v in views)
         assert set(ref) == set(eager) == set(replay)
         for k in ref:
-            assert torch.equal(eager[k], ref[k]), k
-            assert torch.equal(replay[k], ref[k]), k
+            assert torch.equal(eager[k], 2.0 * ref[k]), k
+            assert torch.equal(replay[k], 2.0 * ref[k]), k
         assert red.last_fallback == []
     finally:
         red.close()
@@ -140,6 +160,7 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(400)  # the oracle's full 64-clip encoder step on the host (~1-2 min)
 def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
     """BASELINE config 4's shape in one process: the config-3 encoder (3 streams + residual +
     fusion) at B = 64 = 8 shards x 8 clips.  The eight shards' HIP gradients summed equal

@@ -5,6 +5,7 @@
 export TMPDIR=/tmp
 out=gpurun_out/${1:-pmc_traffic}
 mkdir -p $out
+python3 -c "from scattennet_amd import _lib; print(_lib.source_digest())" > $out/digest.txt
 ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_EXTRA}"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out -o fetch -- python3 $ARGS > $out/fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out -o write -- python3 $ARGS > $out/write.log 2>&1 || exit $?
