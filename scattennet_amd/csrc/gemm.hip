@@ -858,6 +858,285 @@ __global__ __launch_bounds__(512) void gemm_glds2_kernel(const GemmArgs args) {
   epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 }
 
+// ------------------------------------------------------------------------------ TN, large tiles
+// The weight-gradient layout dW[M = out][N = in] = alpha * sum_k A[k][m] B[k][n] (A = dY,
+// B = X, both row-major (M_red, .) with the reduction over their ROWS): both operand tiles
+// are k-major [32 k][rows] LDS images filled by LDS-DMA straight from the row-major
+// activations (lane-linear pieces, no swizzle: a half-wave's fragment read is 32 (or 64 /
+// 128) consecutive floats of one k-row — conflict-free).  Against the 64x64 / 4-wave kernel:
+//   * bigger workgroup tiles (128 x 64, 128 x 128): 21-32 FLOP per staged byte instead of 16,
+//     so half the L2 -> LDS traffic per MFMA and fewer split-K partial slabs for the same fill;
+//   * wave tiles of up to 64 x 64 read by ds_read_b64 / b128: the rows of MFMA block i are the
+//     wave's rows RM*r + i (a free row permutation, undone in the epilogue), so one 8-/16-byte
+//     read feeds RM blocks — 2-4x fewer LDS reads per MFMA than 32x32 wave tiles;
+//   * a ring of S stages with a counted vmcnt that keeps S-2 slices in flight across the
+//     slice barrier (S = 3, 4; the 64x64 kernel's 2-stage ring waits for vmcnt(0) every slice);
+//   * split-K combined in the launch as gemm_glds_kernel does (write-through slabs, arrival
+//     ticket, the last arriver sums the slabs in slice order — deterministic), except that the
+//     last arriver takes its own partial from registers instead of re-reading its slab.
+// Requirements: tn_ok (every split-K chunk a multiple of 32 rows, M and N multiples of 4, one
+// alpha per problem) and vec_ok.
+template <int BM_, int BN_, int WM_, int WN_, int S_>
+struct TnCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
+  static constexpr int RM = TM / 32, RN = TN / 32;  // 32x32 MFMA blocks per wave
+  static constexpr int A_BYTES = GL_BK * BM * 4, B_BYTES = GL_BK * BN * 4, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_PC = A_BYTES / GL_PIECE, B_PC = B_BYTES / GL_PIECE;  // DMA pieces per slice
+  static constexpr int PPW = (A_PC + B_PC) / NW;                                // ... per wave
+  static constexpr int SCR_LD = TN + 4;                                         // epilogue scratch row
+  static constexpr int SCR_BYTES = TM * SCR_LD * 4;                             // ... per wave
+  static constexpr int RING = S * STAGE, SCR = NW * SCR_BYTES;
+  static constexpr int SMEM = (RING > SCR ? RING : SCR) + 16;                   // + the ticket flag
+  static constexpr int Q = TM * TN / 256;  // float4 row pieces per lane in the epilogue
+  static_assert((A_PC + B_PC) % NW == 0, "DMA pieces must divide among the waves");
+  static_assert((RM == 1 || RM == 2 || RM == 4) && (RN == 1 || RN == 2 || RN == 4), "wave tile");
+  static_assert(TN % 4 == 0 && 256 % TN == 0, "row pieces");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+// RM floats at consecutive addresses (the RM MFMA blocks' operands of one lane at one k)
+template <int R>
+__device__ __forceinline__ void tn_read(const float* p, float (&o)[R]) {
+  if constexpr (R == 1) {
+    o[0] = p[0];
+  } else if constexpr (R == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    o[0] = v.x;
+    o[1] = v.y;
+  } else {
+    const f32x4 v = ld4(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = v[i];
+  }
+}
+
+// epilogue_rows' per-row-piece arithmetic for one float4 of row m, columns n .. n+3
+__device__ __forceinline__ void epilogue_row4(const sca_gemm_problem& P, int m, int n, f32x4 v, const DropMask& dm) {
+  const f32x4 bias = P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 ex = {0.f, 0.f, 0.f, 0.f}, ax = ex;
+  if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
+  if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
+  if (P.epi & SCA_EPI_DGELU) ax = ld4(P.aux + (long)m * P.ldx + n);
+  f32x4 o = (v + bias) * P.post_scale;
+  if (P.epi & SCA_EPI_GELU) {
+    st4(P.aux_out + (long)m * P.ldo + n, o);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
+  }
+  if (P.epi & SCA_EPI_DROPOUT) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), o[j]);
+  }
+  if (P.epi & SCA_EPI_DGELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
+  }
+  st4(P.C + (long)m * P.ldc + n, o + ex);
+}
+
+template <class C>
+__global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
+  constexpr int BM = C::BM, BN = C::BN, S = C::S, RM = C::RM, RN = C::RN, TM = C::TM, TN = C::TN;
+  constexpr int PPW = C::PPW, Q = C::Q;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
+  const int splitk = args.splitk;
+  const int pid = bz / splitk, ks = bz % splitk;
+  const sca_gemm_problem& P = args.p[pid];
+  const int m0 = by * BM, n0 = bx * BN;
+  if (m0 >= P.M || n0 >= P.N) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave / C::WN) * TM, wn = (wave % C::WN) * TN;
+  const sca_gemm_seg& G = P.seg[0];
+
+  int kbeg = 0, kend = G.K;
+  if (splitk > 1) {
+    const int chunk = ((G.K + splitk - 1) / splitk + GL_BK - 1) / GL_BK * GL_BK;
+    kbeg = ks * chunk;
+    kend = min(G.K, kbeg + chunk);
+  }
+  const int total = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
+
+  // this wave's DMA pieces: piece q < A_PC is rows 256/BM*q .. of the A image, else of B
+  const float* src[PPW];
+  int dst[PPW];
+  long step[PPW];
+#pragma unroll
+  for (int c = 0; c < PPW; ++c) {
+    const int q = wave * PPW + c;
+    const bool isA = q < C::A_PC;
+    const int rows = isA ? BM : BN, qq = isA ? q : q - C::A_PC;
+    const int kr = qq * (256 / rows) + lane / (rows / 4), col = 4 * (lane % (rows / 4));
+    const float* base = isA ? G.A : G.B;
+    const int ld = isA ? G.lda : G.ldb;
+    const int r0 = isA ? m0 : n0, nr = isA ? P.M : P.N;
+    src[c] = base + (long)(kbeg + kr) * ld + min(r0 + col, nr - 4);
+    dst[c] = (isA ? 0 : C::A_BYTES) + qq * GL_PIECE;
+    step[c] = (long)GL_BK * ld;
+  }
+  auto dma = [&](int t, int stage) {
+    char* b = smem + stage * C::STAGE;
+#pragma unroll
+    for (int c = 0; c < PPW; ++c) gl_dma(src[c] + t * step[c], b + dst[c]);
+  };
+
+  const bool do_bias = P.bias_grad != nullptr && bx == 0 && wn == 0;
+  float bsum[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) bsum[i] = 0.f;
+  f32x16 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < total) dma(i, i);
+  for (int t = 0; t < total; ++t) {
+    if (t + S - 2 < total) gl_wait_vm<PPW * (S - 2)>();
+    else gl_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t-1's stage is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+    const float* As = reinterpret_cast<const float*>(smem + (t % S) * C::STAGE);
+    const float* Bs = As + GL_BK * BM;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float fa[4][RM], fb[4][RN];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 8 * g + 4 * h + j;
+        tn_read<RM>(As + k * BM + wm + RM * r, fa[j]);
+        tn_read<RN>(Bs + k * BN + wn + RN * r, fb[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < RN; ++jj) acc[i][jj] = mfma32(fa[j][i], fb[j][jj], acc[i][jj]);
+      if (do_bias) {  // colsum of dY = row sums of the A image: lane (r, h) holds rows RM r + i
+#pragma unroll
+        for (int i = 0; i < RM; ++i) bsum[i] += (fa[0][i] + fa[1][i]) + (fa[2][i] + fa[3][i]);
+      }
+    }
+  }
+
+  const float alpha = G.alpha;
+  const bool fused_k = splitk > 1 && args.counters != nullptr;
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) bsum[i] += __shfl_xor(bsum[i], 32, 64);  // the two k halves
+    if (h == 0) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int m = m0 + wm + RM * r + i;
+        if (m >= P.M) continue;
+        float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m;
+        if (fused_k)
+          __hip_atomic_store(bp, bsum[i] * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+        else
+          P.bias_grad[m] = bsum[i] * alpha * P.bias_grad_scale;
+      }
+    }
+  }
+  // wave tile -> row pieces through a wave-private LDS scratch (the ring is free once every
+  // wave has passed its last slice); MFMA block (i, jj) row q / column c is the wave's row
+  // RM * q + i / column RN * c + jj (the permuted fragment rows)
+  __syncthreads();
+  float* scr = reinterpret_cast<float*>(smem) + wave * (C::SCR_BYTES / 4);
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < RN; ++jj)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+        scr[(RM * row + i) * C::SCR_LD + RN * r + jj] = acc[i][jj][e] * alpha;
+      }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int LPR = TN / 4;  // lanes per row
+  const int pr = lane / LPR, pc = 4 * (lane % LPR);
+  f32x4 v[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) v[q] = ld4(scr + (pr + q * (64 / LPR)) * C::SCR_LD + pc);
+  const int n = n0 + wn + pc;
+
+  if (fused_k) {
+    const long MN = (long)P.M * P.N;
+    float* slabs = args.ws + args.slab_off[pid];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
+    if (n < P.N) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int m = m0 + wm + pr + q * (64 / LPR);
+        if (m < P.M) {
+          const f32x4 x = v[q];
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs,
+                                                 (int)(((long)ks * MN + (long)m * P.N + n) * 4), 0, 16);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(smem + C::SMEM - 16);
+    unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded: no agent acquire
+    // sum in slice order 0 .. splitk-1, this split's own partial from registers
+    const int nc = min(n, P.N - 4);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const long e = (long)min(m0 + wm + pr + q * (64 / LPR), P.M - 1) * P.N + nc;
+      f32x4 tsum = ks == 0 ? v[q] : ld4_sc1(rs, e);
+      for (int s2 = 1; s2 < splitk; ++s2) tsum += s2 == ks ? v[q] : ld4_sc1(rs, s2 * MN + e);
+      v[q] = tsum;
+    }
+    if (P.bias_grad && bx == 0 && threadIdx.x < BM && m0 + (int)threadIdx.x < P.M) {
+      const float* bp = args.ws + args.bias_off[pid] + m0 + threadIdx.x;
+      float tb = 0.f;
+      for (int s2 = 0; s2 < splitk; ++s2)
+        tb += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P.bias_grad[m0 + threadIdx.x] = tb * P.bias_grad_scale;
+    }
+  } else if (splitk > 1) {  // two-launch form: plain slabs, splitk_reduce4_kernel combines
+    if (n < P.N) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int m = m0 + wm + pr + q * (64 / LPR);
+        if (m < P.M) st4(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N + (long)m * P.N + n, v[q]);
+      }
+    }
+    return;
+  }
+  if (n >= P.N) return;
+  DropMask dm;
+  if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int m = m0 + wm + pr + q * (64 / LPR);
+    if (m < P.M) epilogue_row4(P, m, n, v[q], dm);
+  }
+}
+
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -1770,9 +2049,45 @@ bool vec_ok(const GemmArgs& a, int nprob, int layout) {
   return true;
 }
 
+// large-tile weight-gradient kernels (gemm_tn_kernel), index = tile - 30
+using TN0 = TnCfg<64, 64, 2, 2, 4>;     // 4 waves, 32x32 each, 4-stage ring
+using TN1 = TnCfg<128, 64, 4, 2, 3>;    // 8 waves, 32x32 each
+using TN2 = TnCfg<128, 128, 2, 4, 3>;   // 8 waves, 64x32 each
+using TN3 = TnCfg<128, 128, 2, 2, 3>;   // 4 waves, 64x64 each
+using TN4 = TnCfg<128, 64, 2, 2, 3>;    // 4 waves, 64x32 each
+using TN5 = TnCfg<64, 128, 2, 2, 3>;    // 4 waves, 32x64 each
+constexpr int kTnFirst = 30, kTnLast = 35;
+
+template <class C>
+int launch_tn(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  dim3 grid((maxN + C::BN - 1) / C::BN, (maxM + C::BM - 1) / C::BM, nprob * a.splitk);
+  hipLaunchKernelGGL((gemm_tn_kernel<C>), grid, dim3(C::NT), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
+bool tn_ok(const GemmArgs& a, int nprob) {
+  for (int i = 0; i < nprob; ++i)
+    if (a.p[i].nseg != 1) return false;
+  return glds_ok(a, nprob);
+}
+
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
+  if (tile >= kTnFirst && tile <= kTnLast) {
+    if (LAYOUT != SCA_GEMM_TN || !tn_ok(a, nprob)) {
+      tile = 21;
+    } else {
+      switch (tile) {
+        case 30: return launch_tn<TN0>(a, nprob, maxM, maxN, st);
+        case 31: return launch_tn<TN1>(a, nprob, maxM, maxN, st);
+        case 32: return launch_tn<TN2>(a, nprob, maxM, maxN, st);
+        case 33: return launch_tn<TN3>(a, nprob, maxM, maxN, st);
+        case 34: return launch_tn<TN4>(a, nprob, maxM, maxN, st);
+        default: return launch_tn<TN5>(a, nprob, maxM, maxN, st);
+      }
+    }
+  }
   if (tile > 10 && tile < 20 && !persistent_ok(a, nprob)) tile = 1;
   if (tile >= 20 && !glds_ok(a, nprob)) tile = LAYOUT == SCA_GEMM_TN ? 5 : (LAYOUT == SCA_GEMM_NN ? 7 : 1);
   switch (tile) {
@@ -1824,7 +2139,8 @@ extern "C" int sca_gemm_stamps(unsigned long long* out, int n) {
 #endif
 
 extern "C" int sca_gemm_tile_override(int layout, int tile) {
-  if (layout < 0 || layout > 2 || tile < 0 || (tile > kNumTiles && (tile < 11 || tile > 16) && (tile < 20 || tile > 24)))
+  if (layout < 0 || layout > 2 || tile < 0 ||
+      (tile > kNumTiles && (tile < 11 || tile > 16) && (tile < 20 || tile > 24) && (tile < kTnFirst || tile > kTnLast)))
     return SCA_ERR_ARG;
   g_tile_override[layout] = tile;
   return SCA_OK;
@@ -1901,7 +2217,8 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
   const int tile = pick_tile(layout, tiles64, splitk);
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
-  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22) && glds_ok(a, nprob) &&
+  const bool tn_big = layout == SCA_GEMM_TN && tile >= kTnFirst && tile <= kTnLast && tn_ok(a, nprob);
+  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&
       vec_ok(a, nprob, layout)) {
     a.counters = counters;
     do_reduce = false;

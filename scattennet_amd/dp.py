@@ -247,17 +247,17 @@ class GradBuckets:
         if self.average:
             self.flat.mul_(1.0 / self.world)
 
-    def quiesce(self, seconds=0.5):
-        """Call before capturing a step into a hipGraph: completes every eager collective and
-        gives ProcessGroupNCCL's watchdog thread (it polls every 100 ms) time to retire them
-        — a watchdog query of a pending eager work's event while the graph is being captured
-        aborts the process (tools/dp_capture_diag.py, variant "reducer")."""
-        import time
+    def quiesce(self):
+        """Call before capturing a step into a hipGraph: completes every eager kernel and
+        collective of the warm-up.  Capture then runs in `thread_local` mode, in which the
+        calls ProcessGroupNCCL's watchdog thread makes on the warm-up collectives' events
+        (cudaEventQuery from ITS thread) are legal; no collective is issued here (a barrier
+        would be one more eager work for the watchdog to poll), and nothing of the warm-up's
+        autograd graphs may be alive (the caller drops its outputs: a captured backward that
+        reused a warm-up AccumulateGrad node would fork into the warm-up's stream).  The
+        captured collectives themselves are never handed to the watchdog (ProcessGroupNCCL
+        does not track work enqueued while the stream is capturing)."""
         torch.cuda.synchronize()
-        if dist.is_initialized():
-            dist.barrier()
-        torch.cuda.synchronize()
-        time.sleep(seconds)
 
     def bucket_sizes(self):
         return [n * 4 for _, n, _ in (self.plan or [])]

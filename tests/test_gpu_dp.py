@@ -191,9 +191,9 @@ def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
         out = enc(kp[sl], mask[sl])[0]
         out.backward(gout[0, sl].contiguous())
         torch.cuda.synchronize()
-        # per-clip forward of the shard = the full batch's rows (tile shapes may differ with M:
-        # summation order only)
-        assert rel_err(out, fuse[sl]) < 1e-5, s
+        # per-clip forward of the shard = the full batch's rows, to within summation order
+        # (the GEMM + LayerNorm row tile is 16 rows at 8 clips, 32 at 64; four layers deep)
+        assert rel_err(out, fuse[sl]) < 1e-4, (s, rel_err(out, fuse[sl]))
         for k, p in named.items():
             if p.grad is not None:
                 shard_sum[k] = shard_sum[k] + p.grad if k in shard_sum else p.grad.detach().clone()
