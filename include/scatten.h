@@ -221,7 +221,7 @@ int sca_gemm_tile_override(int layout, int tile);
  * h*hd .. h*hd+hd-1, row stride ld*).  Scores use q as given (the projection already
  * applied hd^-0.5).  Masking, per query row i and key j:
  *   causal && j > i                    -> -inf            (attention.py:165-169)
- *   add_mask != NULL                   -> s + add_mask[b, i, j]   (general (B,1,Tq,Tk))
+ *   add_mask != NULL                   -> s + add_mask[b, (h,) i, j]   (general (B,1|H,Tq,Tk))
  *   else key_valid != NULL && !valid_j -> finfo.min       (utils.py:3-12)
  *   else                               -> s + (causal && plus_one ? 1 : 0) (utils.py:24-27)
  * Softmax stats are saved per (g,b,h,i) in the base-2 domain the kernels compute in
@@ -244,6 +244,9 @@ typedef struct {
    * softmax statistics are those of P.  The backward must get the same seed and p.        */
   unsigned long long drop_seed;
   float drop_p;
+  /* add_mask layout: 0 or 1 = [B, Tq, Tk] shared by every head; H = [B, H, Tq, Tk], one mask
+   * per head (the reference adds any mask broadcastable to (B, H, Tq, Tk), attention.py:65) */
+  int mask_heads;
 } sca_attn_fwd_problem;
 
 typedef struct {
@@ -267,6 +270,7 @@ typedef struct {
                      fixed-order dQ reduction; without it the split dq / dkdv kernels */
   unsigned long long drop_seed; /* the forward's attention-probability dropout */
   float drop_p;
+  int mask_heads;               /* as sca_attn_fwd_problem */
 } sca_attn_bwd_problem;
 
 #define SCA_ATTN_MAX_PROBLEMS 8

@@ -44,14 +44,15 @@ class GemmProblem(ctypes.Structure):
 class AttnFwdProblem(ctypes.Structure):
     _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("stat_m", c_void_p),
                 ("stat_ll", c_void_p), ("key_valid", c_void_p), ("add_mask", c_void_p), ("drop_seed", ctypes.c_uint64),
-                ("drop_p", c_float)]
+                ("drop_p", c_float), ("mask_heads", c_int)]
 
 
 class AttnBwdProblem(ctypes.Structure):
     _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("dout", c_void_p),
                 ("stat_m", c_void_p), ("stat_ll", c_void_p), ("key_valid", c_void_p), ("add_mask", c_void_p),
                 ("dq", c_void_p), ("dk", c_void_p), ("dv", c_void_p), ("delta", c_void_p), ("dq_scale", c_float),
-                ("dv_scale", c_float), ("dq_part", c_void_p), ("drop_seed", ctypes.c_uint64), ("drop_p", c_float)]
+                ("dv_scale", c_float), ("dq_part", c_void_p), ("drop_seed", ctypes.c_uint64), ("drop_p", c_float),
+                ("mask_heads", c_int)]
 
 
 class LnFwdProblem(ctypes.Structure):

@@ -50,15 +50,16 @@ class BaseAttention(nn.Module):
                 self.v_proj.weight, self.v_proj.bias]
 
 
-def _resolve_mask(mask, causal, B, Tq, Tk, device):
+def _resolve_mask(mask, causal, B, Tq, Tk, device, H=1):
     """-> (key_valid, add_mask, plus_one).
 
-    The kernels read `add_mask` as a dense contiguous (B, Tq, Tk) fp32 buffer and
-    `key_valid` as (B, Tk).  The reference adds the mask with `attn_weights += attention_mask`
-    (attention.py:65/117/171), so every mask broadcastable to (B, 1, Tq, Tk) is legal there:
-    (B,1,Tq,Tk), (1,1,Tq,Tk), (B,1,1,Tk), (Tq,Tk), (Tk,), a scalar ...  Such masks are
-    expanded to (B, Tq, Tk) here; per-head masks (dim 1 = H > 1) are not supported
-    (ValueError).  `None` raises TypeError as `attn_weights += None` does."""
+    The kernels read `add_mask` as a dense contiguous (B, Tq, Tk) fp32 buffer (one mask for
+    every head) or (B, H, Tq, Tk) (one per head), and `key_valid` as (B, Tk).  The reference
+    adds the mask with `attn_weights += attention_mask` (attention.py:65/117/171), so every
+    mask broadcastable to (B, H, Tq, Tk) is legal there: (B,1,Tq,Tk), (B,H,Tq,Tk),
+    (1,1,Tq,Tk), (B,1,1,Tk), (Tq,Tk), (Tk,), a scalar ...  Such masks are expanded here to
+    (B, Tq, Tk) when dim 1 is 1, to (B, H, Tq, Tk) when it is H.  `None` raises TypeError
+    as `attn_weights += None` does."""
     if mask is None:
         raise TypeError("unsupported operand type(s) for +=: 'Tensor' and 'NoneType'")
     if isinstance(mask, ops.KeyPaddingMask):
@@ -77,15 +78,15 @@ def _resolve_mask(mask, causal, B, Tq, Tk, device):
                 raise RuntimeError(f"attention_mask on {m.device}, queries on {device}")
             m = m.to(device)
         m = m.reshape((1,) * (4 - m.dim()) + tuple(m.shape))
-        if m.shape[1] != 1:
-            raise ValueError(f"attention_mask of shape {tuple(mask.shape)}: per-head masks are not supported "
-                             "(dim 1 must be 1)")
-        for have, want, name in ((m.shape[0], B, "B"), (m.shape[2], Tq, "Tq"), (m.shape[3], Tk, "Tk")):
+        for have, want, name in ((m.shape[0], B, "B"), (m.shape[1], H, "H"), (m.shape[2], Tq, "Tq"),
+                                 (m.shape[3], Tk, "Tk")):
             if have not in (1, want):
                 raise ValueError(f"attention_mask of shape {tuple(mask.shape)} does not broadcast to "
-                                 f"(B, 1, Tq, Tk) = {(B, 1, Tq, Tk)} ({name})")
-        m = m.to(torch.float32).expand(B, 1, Tq, Tk)[:, 0]
-        return None, m.contiguous(), False
+                                 f"(B, H, Tq, Tk) = {(B, H, Tq, Tk)} ({name})")
+        m = m.to(torch.float32)
+        if m.shape[1] == 1 or H == 1:
+            return None, m.expand(B, 1, Tq, Tk)[:, 0].contiguous(), False
+        return None, m.expand(B, H, Tq, Tk).contiguous(), False
     raise TypeError(f"unsupported attention_mask type {type(mask)}")
 
 
@@ -115,7 +116,8 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
     if hq.dim() != 3:
         raise ValueError(f"hidden_states must be (B, T, d_model), got {tuple(hq.shape)}")
     Tk = kv[0].shape[1] if kind == "cross" else hq.shape[1]
-    key_valid, add_mask, plus_one = _resolve_mask(mask, causal, hq.shape[0], hq.shape[1], Tk, hq.device)
+    key_valid, add_mask, plus_one = _resolve_mask(mask, causal, hq.shape[0], hq.shape[1], Tk, hq.device,
+                                                  a0.num_heads)
     params = []
     for a in attns:
         params += a.qkv_params()

@@ -83,6 +83,12 @@ __device__ __forceinline__ float kv_load(const float* key_valid, int b, int j, i
 }
 
 // per-key additive term in the base-2 domain (see header comment)
+// (clip, head) slice of a materialised additive mask: [B, Tq, Tk] (mask_heads 0 / 1) or
+// [B, H, Tq, Tk] (mask_heads = H)
+__device__ __forceinline__ long mask_clip(int mask_heads, int b, int H, int h) {
+  return mask_heads > 1 ? (long)b * H + h : (long)b;
+}
+
 __device__ __forceinline__ float key_add(float kv, bool add_mask, int j, int Tk, float plus2) {
   if (j >= Tk) return -INFINITY;
   if (add_mask) return 0.f;
@@ -212,7 +218,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const FwdArgs a) {
       for (int j = 0; j < 4; ++j) qreg[s + j] = v[j];
     }
   }
-  const float* amrow = ADDMASK ? P.add_mask + ((long)b * a.Tq + min(qrow, a.Tq - 1)) * a.Tk : nullptr;
+  const float* amrow = ADDMASK ? P.add_mask + (mask_clip(P.mask_heads, b, a.H, h) * a.Tq + min(qrow, a.Tq - 1)) * a.Tk
+                               : nullptr;
 
   f32x4 o[ND];
 #pragma unroll
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   const long si = ((long)b * a.H + h) * a.Tq + qc;
   const float mrow = P.stat_m[si], llrow = P.stat_ll[si];
   if (qok && grp == 0) P.delta[si] = delta;
-  const float* amrow = ADDMASK ? P.add_mask + ((long)b * a.Tq + qc) * a.Tk : nullptr;
+  const float* amrow = ADDMASK ? P.add_mask + (mask_clip(P.mask_heads, b, a.H, h) * a.Tq + qc) * a.Tk : nullptr;
   DropMask dm;
   if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
   const uint32_t erow = drop_row(b, a.H, h, a.Tq, a.Tk, qrow);
@@ -589,7 +596,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
         float t2;
         if (ADDMASK) {
           const int q = min(qb + ql + r, a.Tq - 1);
-          t2 = to_log2(s_acc[r] + (kok ? P.add_mask[((long)b * a.Tq + q) * a.Tk + krow] : 0.f) + kadd);
+          t2 = to_log2(s_acc[r] + (kok ? P.add_mask[(mask_clip(P.mask_heads, b, a.H, h) * a.Tq + q) * a.Tk + krow] : 0.f) +
+                       kadd);
         } else {
           t2 = fmaf(s_acc[r], L2E, kadd);
         }
@@ -1201,6 +1209,10 @@ extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B,
       return SCA_ERR_ARG;
     }
     am = probs[i].add_mask != nullptr;
+    if (probs[i].mask_heads < 0 || (probs[i].mask_heads > 1 && probs[i].mask_heads != H)) {
+      sca_set_error("sca_attn_fwd: mask_heads must be 0, 1 or H");
+      return SCA_ERR_ARG;
+    }
     if (!(probs[i].drop_p >= 0.f && probs[i].drop_p < 1.f)) {
       sca_set_error("sca_attn_fwd: drop_p must be in [0, 1)");
       return SCA_ERR_ARG;
@@ -1241,6 +1253,10 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
       return SCA_ERR_ARG;
     }
     am = p.add_mask != nullptr;
+    if (p.mask_heads < 0 || (p.mask_heads > 1 && p.mask_heads != H)) {
+      sca_set_error("sca_attn_bwd: mask_heads must be 0, 1 or H");
+      return SCA_ERR_ARG;
+    }
     if ((p.dq_part != nullptr) != (probs[0].dq_part != nullptr)) {
       sca_set_error("sca_attn_bwd: all problems must agree on dq_part");
       return SCA_ERR_ARG;

@@ -833,6 +833,11 @@ class KeyPaddingMask:
         return self.mask.shape
 
 
+def _mask_heads(add_mask):
+    """add_mask (B, Tq, Tk) -> 1 (one mask for every head); (B, H, Tq, Tk) -> H."""
+    return add_mask.shape[1] if add_mask is not None and add_mask.dim() == 4 else 1
+
+
 def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
     """drop: None or (p, seeds) — attention-probability dropout, one seed per problem."""
     B, Tq, d = q[0].shape
@@ -846,7 +851,7 @@ def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
         arr = (L.AttnFwdProblem * len(gs))(*[
             L.AttnFwdProblem(q[g].data_ptr(), k[g].data_ptr(), v[g].data_ptr(), o[g].data_ptr(),
                              sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask),
-                             drop[1][g] if drop else 0, drop[0] if drop else 0.0) for g in gs])
+                             drop[1][g] if drop else 0, drop[0] if drop else 0.0, _mask_heads(add_mask)) for g in gs])
         fl = len(gs) * 4.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
         with _timed("attn_fwd_kernel<%d>" % hd, fl):
             L.check(L.lib().sca_attn_fwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
@@ -873,7 +878,8 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
                              dout[g].data_ptr(), sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid),
                              ptr(add_mask), dq[g].data_ptr(), dk[g].data_ptr(), dv[g].data_ptr(),
                              delta[g].data_ptr(), dq_scale, dv_scale, ptr(part[g]),
-                             drop[1][g] if drop else 0, drop[0] if drop else 0.0) for g in gs])
+                             drop[1][g] if drop else 0, drop[0] if drop else 0.0, _mask_heads(add_mask))
+            for g in gs])
         fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
         with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
             L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),

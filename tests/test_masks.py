@@ -1,11 +1,12 @@
 """Attention-mask contract at the drop-in boundary (model/attention.py:65/117/171:
 `attn_weights += attention_mask`).
 
-Every additive mask the reference accepts — anything broadcastable to (B, 1, Tq, Tk) — is
-expanded to the kernels' dense (B, Tq, Tk) layout before a launch; shapes the reference would
-reject (or that the kernels cannot take: per-head masks) raise; `None` raises TypeError as
-`attn_weights += None` does.  CPU tests cover the host-side resolution; the GPU test runs the
-four broadcast shapes through the HIP kernels against the oracle.
+Every additive mask the reference accepts — anything broadcastable to (B, H, Tq, Tk) — is
+expanded to the kernels' dense layout before a launch: (B, Tq, Tk) when it is the same for
+every head, (B, H, Tq, Tk) when it is per head (mask_heads = H in the C ABI); shapes the
+reference would reject raise; `None` raises TypeError as `attn_weights += None` does.  CPU
+tests cover the host-side resolution; the GPU test runs the broadcast shapes, per-head ones
+included, through the HIP kernels against the oracle.
 """
 import pytest
 import torch
@@ -16,9 +17,9 @@ from tests.golden_util import close, rel_err
 PARITY_TOL = 1e-3
 
 
-def _resolve(mask, causal=False, B=3, Tq=5, Tk=7):
+def _resolve(mask, causal=False, B=3, Tq=5, Tk=7, H=4):
     from scattennet_amd.attention import _resolve_mask
-    return _resolve_mask(mask, causal, B, Tq, Tk, torch.device("cpu"))
+    return _resolve_mask(mask, causal, B, Tq, Tk, torch.device("cpu"), H)
 
 
 @pytest.mark.parametrize("shape", [(3, 1, 5, 7), (1, 1, 5, 7), (3, 1, 1, 7), (5, 7), (7,), (1, 5, 1), ()])
@@ -29,6 +30,15 @@ def test_broadcast_masks_expand_to_dense(shape):
     assert am.shape == (3, 5, 7) and am.is_contiguous() and am.dtype == torch.float32
     want = m.reshape((1,) * (4 - m.dim()) + tuple(m.shape)).expand(3, 1, 5, 7)[:, 0]
     assert torch.equal(am, want)
+
+
+@pytest.mark.parametrize("shape", [(3, 4, 5, 7), (1, 4, 5, 7), (3, 4, 1, 7), (4, 1, 1)])
+def test_per_head_masks_expand_to_dense(shape):
+    m = torch.randn(shape)
+    kv, am, plus = _resolve(m)
+    assert kv is None and not plus
+    assert am.shape == (3, 4, 5, 7) and am.is_contiguous()
+    assert torch.equal(am, m.reshape((1,) * (4 - m.dim()) + tuple(m.shape)).expand(3, 4, 5, 7))
 
 
 @pytest.mark.parametrize("shape", [(3, 2, 5, 7), (2, 1, 5, 7), (3, 1, 4, 7), (5, 6), (1, 3, 1, 5, 7)])
@@ -58,7 +68,7 @@ def test_bool_and_int_masks_add_like_the_reference():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["self", "causal", "cross"])
-@pytest.mark.parametrize("form", ["B1TT", "11TT", "B11T", "TT"])
+@pytest.mark.parametrize("form", ["B1TT", "11TT", "B11T", "TT", "BHTT", "1HTT"])
 def test_gpu_broadcast_masks_vs_oracle(kind, form):
     import scattennet_amd as S
     if not torch.cuda.is_available():
@@ -73,7 +83,8 @@ def test_gpu_broadcast_masks_vs_oracle(kind, form):
         for p in m.parameters():
             p.copy_(torch.randn_like(p) / (p.shape[-1] ** 0.5 if p.dim() == 2 else 10.0))
     m = m.to(dev)
-    shape = {"B1TT": (B, 1, Tq, Tk), "11TT": (1, 1, Tq, Tk), "B11T": (B, 1, 1, Tk), "TT": (Tq, Tk)}[form]
+    shape = {"B1TT": (B, 1, Tq, Tk), "11TT": (1, 1, Tq, Tk), "B11T": (B, 1, 1, Tk), "TT": (Tq, Tk),
+             "BHTT": (B, H, Tq, Tk), "1HTT": (1, H, Tq, Tk)}[form]
     # additive masks in the reference's vocabulary: finfo.min on dropped keys, small offsets elsewhere
     am = torch.randn(shape) * 0.5
     drop = torch.rand(shape) < 0.3
