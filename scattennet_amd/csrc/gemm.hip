@@ -876,21 +876,24 @@ __global__ __launch_bounds__(512) void gemm_glds2_kernel(const GemmArgs args) {
 //     last arriver takes its own partial from registers instead of re-reading its slab.
 // Requirements: tn_ok (every split-K chunk a multiple of 32 rows, M and N multiples of 4, one
 // alpha per problem) and vec_ok.
-template <int BM_, int BN_, int WM_, int WN_, int S_>
+template <int BM_, int BN_, int WM_, int WN_, int S_, int LW_ = 0>
 struct TnCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_;
-  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int NW = WM * WN;      // compute waves
+  static constexpr int LW = LW_;          // loader waves (0: the compute waves issue the DMA)
+  static constexpr int NT = 64 * (NW + LW);
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int RM = TM / 32, RN = TN / 32;  // 32x32 MFMA blocks per wave
   static constexpr int A_BYTES = GL_BK * BM * 4, B_BYTES = GL_BK * BN * 4, STAGE = A_BYTES + B_BYTES;
   static constexpr int A_PC = A_BYTES / GL_PIECE, B_PC = B_BYTES / GL_PIECE;  // DMA pieces per slice
-  static constexpr int PPW = (A_PC + B_PC) / NW;                                // ... per wave
+  static constexpr int DW = LW > 0 ? LW : NW;                                   // waves issuing them
+  static constexpr int PPW = (A_PC + B_PC) / DW;                                // ... pieces each
   static constexpr int SCR_LD = TN + 4;                                         // epilogue scratch row
   static constexpr int SCR_BYTES = TM * SCR_LD * 4;                             // ... per wave
   static constexpr int RING = S * STAGE, SCR = NW * SCR_BYTES;
   static constexpr int SMEM = (RING > SCR ? RING : SCR) + 16;                   // + the ticket flag
   static constexpr int Q = TM * TN / 256;  // float4 row pieces per lane in the epilogue
-  static_assert((A_PC + B_PC) % NW == 0, "DMA pieces must divide among the waves");
+  static_assert((A_PC + B_PC) % DW == 0, "DMA pieces must divide among the issuing waves");
   static_assert((RM == 1 || RM == 2 || RM == 4) && (RN == 1 || RN == 2 || RN == 4), "wave tile");
   static_assert(TN % 4 == 0 && 256 % TN == 0, "row pieces");
   static_assert(SMEM <= 160 * 1024, "LDS");
@@ -939,7 +942,7 @@ __device__ __forceinline__ void epilogue_row4(const sca_gemm_problem& P, int m, 
 template <class C>
 __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
   constexpr int BM = C::BM, BN = C::BN, S = C::S, RM = C::RM, RN = C::RN, TM = C::TM, TN = C::TN;
-  constexpr int PPW = C::PPW, Q = C::Q;
+  constexpr int PPW = C::PPW, Q = C::Q, NW = C::NW, LW = C::LW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
 
   const unsigned gx = gridDim.x, gy = gridDim.y;
@@ -954,7 +957,11 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
   const int m0 = by * BM, n0 = bx * BN;
   if (m0 >= P.M || n0 >= P.N) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave / C::WN) * TM, wn = (wave % C::WN) * TN;
+  const bool computes = wave < NW;              // loader waves (wave >= NW) only stream the ring
+  const bool issues = LW == 0 || !computes;     // waves that issue the DMA
+  const int dwave = LW == 0 ? wave : wave - NW;  // index among the issuing waves
+  const int cw = computes ? wave : 0;
+  const int wm = (cw / C::WN) * TM, wn = (cw % C::WN) * TN;
   const sca_gemm_seg& G = P.seg[0];
 
   int kbeg = 0, kend = G.K;
@@ -965,13 +972,13 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
   }
   const int total = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
 
-  // this wave's DMA pieces: piece q < A_PC is rows 256/BM*q .. of the A image, else of B
+  // the issuing wave's DMA pieces: piece q < A_PC is k-rows 256/BM*q .. of the A image, else of B
   const float* src[PPW];
   int dst[PPW];
   long step[PPW];
 #pragma unroll
   for (int c = 0; c < PPW; ++c) {
-    const int q = wave * PPW + c;
+    const int q = dwave * PPW + c;
     const bool isA = q < C::A_PC;
     const int rows = isA ? BM : BN, qq = isA ? q : q - C::A_PC;
     const int kr = qq * (256 / rows) + lane / (rows / 4), col = 4 * (lane % (rows / 4));
@@ -988,7 +995,7 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
     for (int c = 0; c < PPW; ++c) gl_dma(src[c] + t * step[c], b + dst[c]);
   };
 
-  const bool do_bias = P.bias_grad != nullptr && bx == 0 && wn == 0;
+  const bool do_bias = computes && P.bias_grad != nullptr && bx == 0 && wn == 0;
   float bsum[RM];
 #pragma unroll
   for (int i = 0; i < RM; ++i) bsum[i] = 0.f;
@@ -1001,15 +1008,20 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int r = lane & 31, h = lane >> 5;
+  if (issues) {
 #pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < total) dma(i, i);
+    for (int i = 0; i < S - 1; ++i)
+      if (i < total) dma(i, i);
+  }
   for (int t = 0; t < total; ++t) {
-    if (t + S - 2 < total) gl_wait_vm<PPW * (S - 2)>();
-    else gl_wait_vm<0>();
+    if (issues) {  // this wave's pieces of slice t landed (S-2 younger slices may fly)
+      if (t + S - 2 < total) gl_wait_vm<PPW * (S - 2)>();
+      else gl_wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t-1's stage is free
     __builtin_amdgcn_sched_barrier(0);
-    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+    if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+    if (!computes) continue;
     const float* As = reinterpret_cast<const float*>(smem + (t % S) * C::STAGE);
     const float* Bs = As + GL_BK * BM;
 #pragma unroll
@@ -1044,11 +1056,15 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
       for (int i = 0; i < RM; ++i) {
         const int m = m0 + wm + RM * r + i;
         if (m >= P.M) continue;
-        float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m;
-        if (fused_k)
-          __hip_atomic_store(bp, bsum[i] * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-        else
+        if (splitk > 1) {
+          float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m;
+          if (fused_k)
+            __hip_atomic_store(bp, bsum[i] * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+          else
+            *bp = bsum[i] * alpha;
+        } else {
           P.bias_grad[m] = bsum[i] * alpha * P.bias_grad_scale;
+        }
       }
     }
   }
@@ -1056,31 +1072,33 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
   // wave has passed its last slice); MFMA block (i, jj) row q / column c is the wave's row
   // RM * q + i / column RN * c + jj (the permuted fragment rows)
   __syncthreads();
-  float* scr = reinterpret_cast<float*>(smem) + wave * (C::SCR_BYTES / 4);
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int jj = 0; jj < RN; ++jj)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-        scr[(RM * row + i) * C::SCR_LD + RN * r + jj] = acc[i][jj][e] * alpha;
-      }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   constexpr int LPR = TN / 4;  // lanes per row
   const int pr = lane / LPR, pc = 4 * (lane % LPR);
   f32x4 v[Q];
+  if (computes) {
+    float* scr = reinterpret_cast<float*>(smem) + wave * (C::SCR_BYTES / 4);
 #pragma unroll
-  for (int q = 0; q < Q; ++q) v[q] = ld4(scr + (pr + q * (64 / LPR)) * C::SCR_LD + pc);
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < RN; ++jj)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+          scr[(RM * row + i) * C::SCR_LD + RN * r + jj] = acc[i][jj][e] * alpha;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = ld4(scr + (pr + q * (64 / LPR)) * C::SCR_LD + pc);
+  }
   const int n = n0 + wn + pc;
 
   if (fused_k) {
     const long MN = (long)P.M * P.N;
     float* slabs = args.ws + args.slab_off[pid];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
-    if (n < P.N) {
+    if (computes && n < P.N) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int m = m0 + wm + pr + q * (64 / LPR);
@@ -1101,15 +1119,6 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
     if (!*flag) return;
     if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded: no agent acquire
-    // sum in slice order 0 .. splitk-1, this split's own partial from registers
-    const int nc = min(n, P.N - 4);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const long e = (long)min(m0 + wm + pr + q * (64 / LPR), P.M - 1) * P.N + nc;
-      f32x4 tsum = ks == 0 ? v[q] : ld4_sc1(rs, e);
-      for (int s2 = 1; s2 < splitk; ++s2) tsum += s2 == ks ? v[q] : ld4_sc1(rs, s2 * MN + e);
-      v[q] = tsum;
-    }
     if (P.bias_grad && bx == 0 && threadIdx.x < BM && m0 + (int)threadIdx.x < P.M) {
       const float* bp = args.ws + args.bias_off[pid] + m0 + threadIdx.x;
       float tb = 0.f;
@@ -1117,8 +1126,30 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
         tb += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       P.bias_grad[m0 + threadIdx.x] = tb * P.bias_grad_scale;
     }
+    if (!computes) return;
+    // sum in slice order 0 .. splitk-1, this split's own partial from registers; one slab's
+    // Q loads are issued together (one latency per slab, not per float4)
+    const int nc = min(n, P.N - 4);
+    long e[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) e[q] = (long)min(m0 + wm + pr + q * (64 / LPR), P.M - 1) * P.N + nc;
+    f32x4 tsum[Q];
+    for (int s2 = 0; s2 < splitk; ++s2) {
+      f32x4 x[Q];
+      if (s2 == ks) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) x[q] = v[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) x[q] = ld4_sc1(rs, s2 * MN + e[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) tsum[q] = s2 == 0 ? x[q] : tsum[q] + x[q];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = tsum[q];
   } else if (splitk > 1) {  // two-launch form: plain slabs, splitk_reduce4_kernel combines
-    if (n < P.N) {
+    if (computes && n < P.N) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int m = m0 + wm + pr + q * (64 / LPR);
@@ -1127,7 +1158,7 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
     }
     return;
   }
-  if (n >= P.N) return;
+  if (!computes || n >= P.N) return;
   DropMask dm;
   if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
 #pragma unroll
@@ -2050,12 +2081,12 @@ bool vec_ok(const GemmArgs& a, int nprob, int layout) {
 }
 
 // large-tile weight-gradient kernels (gemm_tn_kernel), index = tile - 30
-using TN0 = TnCfg<64, 64, 2, 2, 4>;     // 4 waves, 32x32 each, 4-stage ring
-using TN1 = TnCfg<128, 64, 4, 2, 3>;    // 8 waves, 32x32 each
-using TN2 = TnCfg<128, 128, 2, 4, 3>;   // 8 waves, 64x32 each
-using TN3 = TnCfg<128, 128, 2, 2, 3>;   // 4 waves, 64x64 each
-using TN4 = TnCfg<128, 64, 2, 2, 3>;    // 4 waves, 64x32 each
-using TN5 = TnCfg<64, 128, 2, 2, 3>;    // 4 waves, 32x64 each
+using TN0 = TnCfg<64, 64, 2, 2, 4>;       // 4 waves, 32x32 each, 4-stage ring
+using TN1 = TnCfg<64, 64, 2, 2, 4, 4>;    // + 4 loader waves
+using TN2 = TnCfg<128, 64, 2, 2, 4, 4>;   // 4 compute waves 64x32 + 4 loader waves
+using TN3 = TnCfg<64, 64, 2, 2, 3, 2>;    // 4 compute + 2 loader waves, 3 stages
+using TN4 = TnCfg<128, 64, 4, 2, 3, 4>;   // 8 compute waves 32x32 + 4 loader waves
+using TN5 = TnCfg<128, 128, 2, 2, 3, 4>;  // 4 compute waves 64x64 + 4 loader waves
 constexpr int kTnFirst = 30, kTnLast = 35;
 
 template <class C>
@@ -2277,7 +2308,8 @@ extern "C" int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_probl
 // workgroups / CU): tools/gemm_ln_bench.py 4x(2048,256,K): K = 768 41.0 vs 44.6 us,
 // K = 256 19.8 vs 20.8 us; 1x(2048,256,256): 15.2 vs 10.9 us.  Chained passes: always 32.
 extern "C" int sca_gemm_ln_rows(int nprob, int maxM, int chain) {
-  static const int bm_env = getenv("SCA_GEMM_LN_BM") ? atoi(getenv("SCA_GEMM_LN_BM")) : 0;
+  const char* env = getenv("SCA_GEMM_LN_BM");  // read per call: tests force one tile height
+  const int bm_env = env ? atoi(env) : 0;
   const long wg32 = (long)nprob * ((maxM + 31) / 32);
   if (chain) return 32;
   if (bm_env == 16 || bm_env == 32) return bm_env;

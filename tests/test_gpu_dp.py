@@ -170,6 +170,11 @@ def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
     from tests.test_gpu_scale import hip_encoder_step, tie_aware_encoder_oracle
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
+    # one GEMM + LayerNorm row-tile height for the 8- and the 64-clip launches (the launcher
+    # picks 16 rows at 8 clips, 32 at 64): the shards then compute every clip's forward
+    # exactly as the full batch does, so no ReLU / max-pool rounding tie can resolve
+    # differently between the two and the sums compare at rounding level
+    monkeypatch.setenv("SCA_GEMM_LN_BM", "32")
     dev = torch.device("cuda:0")
     w = dict(W.WORKLOADS["cfg3"], B=64)
     enc = W.build_encoder(w, dev, seed=8, init="random").eval()
@@ -191,9 +196,7 @@ def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
         out = enc(kp[sl], mask[sl])[0]
         out.backward(gout[0, sl].contiguous())
         torch.cuda.synchronize()
-        # per-clip forward of the shard = the full batch's rows, to within summation order
-        # (the GEMM + LayerNorm row tile is 16 rows at 8 clips, 32 at 64; four layers deep)
-        assert rel_err(out, fuse[sl]) < 1e-4, (s, rel_err(out, fuse[sl]))
+        assert torch.equal(out, fuse[sl]), (s, rel_err(out, fuse[sl]))  # the same per-clip forward
         for k, p in named.items():
             if p.grad is not None:
                 shard_sum[k] = shard_sum[k] + p.grad if k in shard_sum else p.grad.detach().clone()

@@ -87,8 +87,9 @@ def _tie_aware_pool(o, gpu_in, stats):
     both computations — and the oracle's own argmax elsewhere (first element on exact
     equality, as torch's MaxPool1d)."""
     dev = _deviation(gpu_in, o.detach(), torch.ones_like(o, dtype=torch.bool), stats)
-    a, b = o[:, 0::2], o[:, 1::2]
-    ga, gb = gpu_in[:, 0::2], gpu_in[:, 1::2]
+    n = o.shape[1] // 2 * 2  # MaxPool1d(2, 2) drops an odd last frame
+    a, b = o[:, 0:n:2], o[:, 1:n:2]
+    ga, gb = gpu_in[:, 0:n:2], gpu_in[:, 1:n:2]
     mine, theirs = b > a, gb > ga
     tie = (a - b).abs() <= 2 * dev
     stats["ties"] += int((tie & (a != b)).sum())
