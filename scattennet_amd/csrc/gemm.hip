@@ -876,9 +876,11 @@ __global__ __launch_bounds__(512) void gemm_glds2_kernel(const GemmArgs args) {
 //     last arriver takes its own partial from registers instead of re-reading its slab.
 // Requirements: tn_ok (every split-K chunk a multiple of 32 rows, M and N multiples of 4, one
 // alpha per problem) and vec_ok.
-template <int BM_, int BN_, int WM_, int WN_, int S_, int LW_ = 0>
+template <int BM_, int BN_, int WM_, int WN_, int S_, int LW_ = 0, bool PF_ = false>
 struct TnCfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_;
+  static constexpr bool PF = PF_;         // fragments read one slice ahead (needs S >= 3)
+  static_assert(!PF || S >= 3, "prefetch needs a 3-stage ring");
   static constexpr int NW = WM * WN;      // compute waves
   static constexpr int LW = LW_;          // loader waves (0: the compute waves issue the DMA)
   static constexpr int NT = 64 * (NW + LW);
@@ -1013,36 +1015,82 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
     for (int i = 0; i < S - 1; ++i)
       if (i < total) dma(i, i);
   }
-  for (int t = 0; t < total; ++t) {
-    if (issues) {  // this wave's pieces of slice t landed (S-2 younger slices may fly)
-      if (t + S - 2 < total) gl_wait_vm<PPW * (S - 2)>();
-      else gl_wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t-1's stage is free
-    __builtin_amdgcn_sched_barrier(0);
-    if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
-    if (!computes) continue;
+  // fragments of a slice in registers: [k-group g][k-step j][block]
+  using FragA = float[4][4][RM];
+  using FragB = float[4][4][RN];
+  auto read_frags = [&](int t, FragA& fa, FragB& fb) {
     const float* As = reinterpret_cast<const float*>(smem + (t % S) * C::STAGE);
     const float* Bs = As + GL_BK * BM;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float fa[4][RM], fb[4][RN];
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 8 * g + 4 * h + j;
-        tn_read<RM>(As + k * BM + wm + RM * r, fa[j]);
-        tn_read<RN>(Bs + k * BN + wn + RN * r, fb[j]);
+        tn_read<RM>(As + k * BM + wm + RM * r, fa[g][j]);
+        tn_read<RN>(Bs + k * BN + wn + RN * r, fb[g][j]);
       }
+  };
+  auto mfmas = [&](const FragA& fa, const FragB& fb) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
-          for (int jj = 0; jj < RN; ++jj) acc[i][jj] = mfma32(fa[j][i], fb[j][jj], acc[i][jj]);
+          for (int jj = 0; jj < RN; ++jj) acc[i][jj] = mfma32(fa[g][j][i], fb[g][j][jj], acc[i][jj]);
       if (do_bias) {  // colsum of dY = row sums of the A image: lane (r, h) holds rows RM r + i
 #pragma unroll
-        for (int i = 0; i < RM; ++i) bsum[i] += (fa[0][i] + fa[1][i]) + (fa[2][i] + fa[3][i]);
+        for (int i = 0; i < RM; ++i) bsum[i] += (fa[g][0][i] + fa[g][1][i]) + (fa[g][2][i] + fa[g][3][i]);
       }
+    }
+  };
+  if constexpr (C::PF) {
+    // fragments one slice ahead: after the barrier that publishes slice t + 1 a compute wave
+    // issues the LDS reads of slice t + 1 and the MFMAs of slice t (its fragments already in
+    // registers), so no LDS latency sits between a barrier and the MFMAs.  The barrier of
+    // iteration t requires slices <= t + 1 landed (S - 3 younger slices in flight) and
+    // every wave done READING slices <= t, so the DMA of slice t + S - 1 may overwrite the
+    // stage of slice t - 1.
+    FragA fa0, fa1;
+    FragB fb0, fb1;
+    if (issues) {
+      if (total >= S - 1) gl_wait_vm<PPW * (S - 2)>();
+      else gl_wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (computes && total > 0) read_frags(0, fa0, fb0);
+    auto iter = [&](int t, FragA& fa_cur, FragB& fb_cur, FragA& fa_nxt, FragB& fb_nxt) {
+      if (issues) {
+        if (t + S - 2 < total) gl_wait_vm<PPW * (S - 3)>();
+        else gl_wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+      if (!computes) return;
+      if (t + 1 < total) read_frags(t + 1, fa_nxt, fb_nxt);
+      mfmas(fa_cur, fb_cur);
+    };
+    for (int t = 0; t < total; t += 2) {
+      iter(t, fa0, fb0, fa1, fb1);
+      if (t + 1 < total) iter(t + 1, fa1, fb1, fa0, fb0);
+    }
+  } else {
+    for (int t = 0; t < total; ++t) {
+      if (issues) {  // this wave's pieces of slice t landed (S-2 younger slices may fly)
+        if (t + S - 2 < total) gl_wait_vm<PPW * (S - 2)>();
+        else gl_wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t-1's stage is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+      if (!computes) continue;
+      FragA fa;
+      FragB fb;
+      read_frags(t, fa, fb);
+      mfmas(fa, fb);
     }
   }
 
@@ -2081,12 +2129,12 @@ bool vec_ok(const GemmArgs& a, int nprob, int layout) {
 }
 
 // large-tile weight-gradient kernels (gemm_tn_kernel), index = tile - 30
-using TN0 = TnCfg<64, 64, 2, 2, 4>;       // 4 waves, 32x32 each, 4-stage ring
-using TN1 = TnCfg<64, 64, 2, 2, 4, 4>;    // + 4 loader waves
-using TN2 = TnCfg<128, 64, 2, 2, 4, 4>;   // 4 compute waves 64x32 + 4 loader waves
-using TN3 = TnCfg<64, 64, 2, 2, 3, 2>;    // 4 compute + 2 loader waves, 3 stages
-using TN4 = TnCfg<128, 64, 4, 2, 3, 4>;   // 8 compute waves 32x32 + 4 loader waves
-using TN5 = TnCfg<128, 128, 2, 2, 3, 4>;  // 4 compute waves 64x64 + 4 loader waves
+using TN0 = TnCfg<64, 64, 2, 2, 4>;             // 4 waves, 32x32 each, 4-stage ring
+using TN1 = TnCfg<64, 64, 2, 2, 4, 4>;          // + 4 loader waves
+using TN2 = TnCfg<64, 64, 2, 2, 4, 0, true>;    // 4 waves, fragments one slice ahead
+using TN3 = TnCfg<64, 64, 2, 2, 4, 4, true>;    // + 4 loader waves, fragments one slice ahead
+using TN4 = TnCfg<128, 64, 2, 2, 4, 4, true>;   // 4 compute waves 64x32 + 4 loaders, prefetch
+using TN5 = TnCfg<64, 64, 2, 2, 3, 4, true>;    // 3 stages + 4 loaders, prefetch
 constexpr int kTnFirst = 30, kTnLast = 35;
 
 template <class C>

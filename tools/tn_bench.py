@@ -17,8 +17,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-NAMES = {21: "glds64", 30: "T64s4", 31: "T64+4L", 32: "T128x64+4L", 33: "T64s3+2L", 34: "T128x64w8+4L", 35: "T128+4L"}
-TILE_BM = {21: (64, 64), 30: (64, 64), 31: (64, 64), 32: (128, 64), 33: (64, 64), 34: (128, 64), 35: (128, 128)}
+NAMES = {21: "glds64", 30: "T64s4", 31: "T64+4L", 32: "T64pf", 33: "T64pf+4L", 34: "T128x64pf+4L", 35: "T64s3pf+4L"}
+TILE_BM = {21: (64, 64), 30: (64, 64), 31: (64, 64), 32: (64, 64), 33: (64, 64), 34: (128, 64), 35: (64, 64)}
 
 
 def make_case(name, shapes, Mr=2048):
