@@ -1070,7 +1070,11 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
       __builtin_amdgcn_sched_barrier(0);
       if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
       if (!computes) return;
-      if (t + 1 < total) read_frags(t + 1, fa_nxt, fb_nxt);
+      // the current fragments' reads (issued an iteration ago) are complete: say so to the
+      // waitcnt pass, which cannot otherwise wait for them behind 16 younger LDS reads (the
+      // lgkmcnt field holds 15) and would wait for the next slice's reads before the MFMAs
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt unconstrained
+      read_frags(t + 1, fa_nxt, fb_nxt);   // past the last slice: a stale stage, never used
       mfmas(fa_cur, fb_cur);
     };
     for (int t = 0; t < total; t += 2) {

@@ -58,3 +58,53 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def calls(enc, kp, mask):
+    """Outputs of every autograd Function of ops, in call order."""
+    from scattennet_amd import ops
+    rec = []
+    saved = {}
+    for cname in ("AttentionBlock", "LinearResidual", "FeedForwardResidual", "LayerNormAdd", "MaxPoolT",
+                  "CoordinateMappingOp", "LinearGelu", "ClipMatmul", "SoftmaxRows"):
+        cls = getattr(ops, cname)
+        fwd = cls.forward
+        saved[cname] = fwd
+
+        def wrap(ctx, *a, _fwd=fwd, _n=cname):
+            out = _fwd(ctx, *a)
+            outs = out if isinstance(out, tuple) else (out,)
+            rec.append((_n, [o.detach().clone() for o in outs if torch.is_tensor(o)]))
+            return out
+        cls.forward = staticmethod(wrap)
+    try:
+        with torch.no_grad():
+            enc(kp, mask)
+    finally:
+        for cname, fwd in saved.items():
+            getattr(ops, cname).forward = staticmethod(fwd)
+    return rec
+
+
+def first_divergence():
+    dev = torch.device("cuda:0")
+    w = dict(W.WORKLOADS["cfg3"], B=64)
+    enc = W.build_encoder(w, dev, seed=8, init="random").eval()
+    kp, mask, _ = W.synthetic_batch(w, dev, seed=12)
+    full = calls(enc, kp, mask)
+    part = calls(enc, kp[:8], mask[:8])
+    for i, ((n1, o1), (n2, o2)) in enumerate(zip(full, part)):
+        for j, (a, b) in enumerate(zip(o1, o2)):
+            a8 = a.reshape(64, -1)[:8] if a.shape[0] == 64 or a.numel() % 64 == 0 else a
+            b8 = b.reshape(8, -1)
+            if a8.shape != b8.shape:
+                continue
+            d = float((a8 - b8).abs().max())
+            if d != 0.0:
+                print(f"call {i} {n1} output {j}: max|diff| {d:.3e}")
+                return
+    print("no divergence")
+
+
+if __name__ == "__main__" and os.environ.get("SHARD_CALLS"):
+    first_divergence()
