@@ -170,11 +170,14 @@ def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
     from tests.test_gpu_scale import hip_encoder_step, tie_aware_encoder_oracle
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    # one GEMM + LayerNorm row-tile height for the 8- and the 64-clip launches (the launcher
-    # picks 16 rows at 8 clips, 32 at 64): the shards then compute every clip's forward
-    # exactly as the full batch does, so no ReLU / max-pool rounding tie can resolve
-    # differently between the two and the sums compare at rounding level
+    # the same kernels for the 8- and the 64-clip launches (the launchers pick 16-row GEMM +
+    # LayerNorm tiles and no chained next-op passes below 256 row tiles): the shards then
+    # compute every clip's forward exactly as the full batch does, so no ReLU / max-pool
+    # rounding tie can resolve differently between the two and the sums compare at rounding
+    # level
     monkeypatch.setenv("SCA_GEMM_LN_BM", "32")
+    from scattennet_amd import ops
+    monkeypatch.setattr(ops, "_CHAIN_MIN_TILES", 0)  # chained next-op passes at 8 clips too
     dev = torch.device("cuda:0")
     w = dict(W.WORKLOADS["cfg3"], B=64)
     enc = W.build_encoder(w, dev, seed=8, init="random").eval()
