@@ -515,6 +515,22 @@ def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
                 "sca_reduce_rows")
 
 
+# weight-gradient kernel experiments: SCA_TN_TILE (sca_gemm_tile_override id for the TN
+# layout: 21 = the 64x64 LDS-DMA kernel, 30-35 = gemm_tn_kernel variants) and SCA_TN_SPLITK
+# (a fixed split-K for every weight-gradient launch; 0 = the _splitk_for rule)
+_TN_TILE = int(__import__("os").environ.get("SCA_TN_TILE", "0"))
+_TN_SPLITK = int(__import__("os").environ.get("SCA_TN_SPLITK", "0"))
+_TN_SET = False
+
+
+def _tn_setup():
+    global _TN_SET
+    if not _TN_SET:
+        _TN_SET = True
+        if _TN_TILE:
+            L.check(L.lib().sca_gemm_tile_override(L.GEMM_TN, _TN_TILE), "sca_gemm_tile_override")
+
+
 def _splitk_for(M_red, n_out_tiles):
     """Split the long reduction (rows of the batch) of weight-gradient GEMMs so that the
     grid covers the 256 CUs about four times (measured best for the concurrent side-stream
@@ -781,7 +797,8 @@ def _weight_grads(items):
         for c in range(0, len(idxs), L.GEMM_MAX_PROBLEMS):
             sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
             tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
-            sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
+            _tn_setup()
+            sk = _TN_SPLITK if _TN_SPLITK > 0 else _splitk_for(items[sub[0]][0].shape[0], tiles)
             probs, wsz = [], 0
             for i in sub:
                 dY, X, alpha, W, _, bscale = items[i]
