@@ -503,10 +503,12 @@ __device__ __forceinline__ f32x4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, long float_o
 // entry, first slice landed, main loop done, epilogue done -> tools/gemm_stamps.py
 constexpr int STAMP_MAX = 16384;
 __device__ unsigned long long g_stamps[STAMP_MAX][5];
+__device__ unsigned long long g_clk[STAMP_MAX][2];  // s_memtime (shader clock) at entry / loop done
 #define SCA_STAMP(slot)                                                            \
   do {                                                                             \
     if (threadIdx.x == 0 && stamp_id < STAMP_MAX) {                                \
       g_stamps[stamp_id][slot] = __builtin_amdgcn_s_memrealtime();                 \
+      if ((slot) == 0 || (slot) == 2) g_clk[stamp_id][(slot) / 2] = __builtin_amdgcn_s_memtime(); \
     }                                                                              \
   } while (0)
 #else
@@ -2218,6 +2220,10 @@ int pick_tile(int layout, long tiles64, int splitk) {
 extern "C" int sca_gemm_stamps(unsigned long long* out, int n) {
   if (n > STAMP_MAX) n = STAMP_MAX;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 5 * n) == hipSuccess ? 0 : 3;
+}
+extern "C" int sca_gemm_clk(unsigned long long* out, int n) {
+  if (n > STAMP_MAX) n = STAMP_MAX;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(unsigned long long) * 2 * n) == hipSuccess ? 0 : 3;
 }
 #endif
 
