@@ -193,12 +193,17 @@ class HipOpError(RuntimeError):
     pass
 
 
+POST_LAUNCH = None  # ops installs a hook run after every successful C-ABI launch
+
+
 def check(rc, what):
     if rc != 0:
         msg = lib().sca_last_error().decode()
         if rc == 1:
             raise ValueError(f"{what}: {msg}")
         raise HipOpError(f"{what} failed ({rc}): {msg}")
+    if POST_LAUNCH is not None:
+        POST_LAUNCH()
 
 
 def stream_handle():

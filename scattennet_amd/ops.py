@@ -723,11 +723,54 @@ def _queue_join(main, side):
     _join_pending[key] = True
 
     def _join():
+        flush_weight_grads()
         _join_pending[key] = False
         main.wait_stream(side)
         note_join(main, side)
 
     torch.autograd.Variable._execution_engine.queue_callback(_join)
+
+
+# Deferred weight-gradient launches (SCA_WGRAD_DEFER=1): the side stream forks from the main
+# stream at once (its dependency set is fixed there), but its kernels are launched only after
+# the NEXT launch on the main stream.  Under graph capture the critical-path kernel is then
+# the first child of its predecessor and the weight gradients the second, so the graph
+# executor's queue assignment (child i -> queue (parent + i) mod N) keeps the
+# critical chain on one hardware queue instead of hopping (and queueing behind a weight-
+# gradient launch) at every fork.
+_WGRAD_DEFER = _os.environ.get("SCA_WGRAD_DEFER", "0") != "0"
+_PENDING_WGRAD = []  # (main stream ptr, side stream, closure)
+_FLUSHING = False
+
+
+def flush_weight_grads(after_stream=None):
+    """Launch the deferred weight-gradient closures (all, or those whose main stream is
+    `after_stream` — called after a launch on that stream)."""
+    global _FLUSHING
+    if _FLUSHING or not _PENDING_WGRAD:
+        return
+    _FLUSHING = True
+    try:
+        keep = []
+        todo = []
+        for ent in _PENDING_WGRAD:
+            (todo if after_stream is None or ent[0] == after_stream else keep).append(ent)
+        _PENDING_WGRAD[:] = keep
+        for _, side, fn in todo:
+            with torch.cuda.stream(side):
+                fn()
+    finally:
+        _FLUSHING = False
+
+
+def _post_launch():
+    if _PENDING_WGRAD and not _FLUSHING:
+        cur = torch.cuda.current_stream().cuda_stream
+        if any(ent[0] == cur for ent in _PENDING_WGRAD):
+            flush_weight_grads(cur)
+
+
+L.POST_LAUNCH = _post_launch
 
 
 def weight_grads(items, M=None, extra=None):
@@ -773,14 +816,29 @@ def weight_grads(items, M=None, extra=None):
         it[1].record_stream(side)
     for t in (extra[1] if extra is not None else ()):
         t.record_stream(side)
-    with torch.cuda.stream(side):
-        out = run()
+    if _WGRAD_DEFER:
+        flush_weight_grads()  # earlier deferred launches keep their order on the side streams
+        with torch.cuda.stream(side):
+            out, launch = _weight_grads(items, deferred=True)
+
+        def later():
+            launch()
+            params_produced([p for it in items for p in (it[3], it[4])])
+            if extra is not None:
+                extra[0]()
+                params_produced(extra[2])
+        _PENDING_WGRAD.append((main.cuda_stream, side, later))
+    else:
+        with torch.cuda.stream(side):
+            out = run()
     _queue_join(join_into, side)
     return out
 
 
-def _weight_grads(items):
+def _weight_grads(items, deferred=False):
+    """Allocate and launch; deferred=True: allocate now, return (out, launch closure)."""
     out = []
+    launches = []
     by_shape = {}  # problems of one launch (SCA_WGRAD_MIX=1: any shapes, one launch)
     items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
     for idx, (dY, X, alpha, W, bias, _) in enumerate(items):
@@ -808,7 +866,11 @@ def _weight_grads(items):
                                    bias_grad=out[i][1], bias_grad_scale=bscale / alpha))
                 wsz += sk * (n_out * n_in + n_out)
             ws = torch.empty(wsz, device=items[0][0].device, dtype=torch.float32) if sk > 1 else None
-            gemm(L.GEMM_TN, probs, splitk=sk, ws=ws)
+            launches.append((probs, sk, ws))
+    if deferred:
+        return out, lambda: [gemm(L.GEMM_TN, p, splitk=k, ws=w) for p, k, w in launches]
+    for p, k, w in launches:
+        gemm(L.GEMM_TN, p, splitk=k, ws=w)
     return out
 
 
