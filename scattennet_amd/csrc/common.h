@@ -34,6 +34,13 @@ __device__ __forceinline__ float wave_max(float v) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+// stores through the GLOBAL address space (global_store_*, counted in order by vmcnt): a
+// generic pointer the compiler cannot resolve becomes a flat_store, which completes out of
+// order with respect to vmcnt — unusable where a counted vmcnt lets stores stay in flight
+typedef __attribute__((address_space(1))) f32x4 g_f32x4;
+typedef __attribute__((address_space(1))) float g_float;
+__device__ __forceinline__ void st4g(float* p, f32x4 v) { *(g_f32x4*)(p) = v; }
+__device__ __forceinline__ void st1g(float* p, float v) { *(g_float*)(p) = v; }
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);

@@ -1290,11 +1290,11 @@ __device__ __forceinline__ void chain_rows(const sca_gemm_chain_pass& Q, const f
     if (m >= M) continue;
     f32x4 o = (v[i] + bias) * Q.post_scale;
     if (Q.epi & SCA_EPI_GELU) {
-      st4(Q.aux_out + (long)m * Q.ldo + n, o);
+      st4g(Q.aux_out + (long)m * Q.ldo + n, o);
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
     }
-    st4(Q.C + (long)m * Q.ldc + n, o);
+    st4g(Q.C + (long)m * Q.ldc + n, o);
   }
 }
 
@@ -1488,11 +1488,11 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     const f32x4 y = (v[i] - mean) * rstd * gam + bet;
     if (CH) st4(reinterpret_cast<float*>(smem + LG_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
     if (m < P.M) {
-      st4(P.C + (long)m * P.ldc + n, v[i]);
-      st4(LN.y + (long)m * LG_BN + n, y);
+      st4g(P.C + (long)m * P.ldc + n, v[i]);
+      st4g(LN.y + (long)m * LG_BN + n, y);
       if (lane == 0) {
-        LN.mean[m] = mean;
-        LN.rstd[m] = rstd;
+        st1g(LN.mean + m, mean);
+        st1g(LN.rstd + m, rstd);
       }
     }
   }
@@ -1508,8 +1508,24 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
     __syncthreads();  // every wave's y rows written to the image
+    // the waits for a slice's DMA let this wave's epilogue stores stay in flight (vmcnt counts
+    // stores too, in issue order): at u = 0 the 16 LayerNorm stores (v, y, mean, rstd of 4
+    // rows) and slice 1's 4 pieces are younger than slice 0; after a pass's epilogue its 4
+    // (8 with GELU) row-piece stores are younger than the next slice.  Exact for full tiles
+    // (every row < M); a partial tile waits for everything.
+    const bool full = m0 + BM <= P.M;
     for (int u = 0; u < nsl; ++u) {
-      gl_wait_vm<0>();
+      if (!full) {
+        gl_wait_vm<0>();
+      } else if (u == 0) {
+        if (nsl > 1) gl_wait_vm<20>();
+        else gl_wait_vm<16>();
+      } else if ((u & 7) == 0) {
+        if (LN.pass[pass_of(u - 1)].epi & SCA_EPI_GELU) gl_wait_vm<8>();
+        else gl_wait_vm<4>();
+      } else {
+        gl_wait_vm<0>();
+      }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
@@ -1717,8 +1733,8 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rs[i];
     if (chain) st4(A2 + lr * LB_A2_LD + n, d);  // rows past M: finite, their products never stored
     if (m < P.M) {
-      st4(P.C + (long)m * P.ldc + n, g[i]);
-      st4(LN.dx + (long)m * LG_BN + n, d);
+      st4g(P.C + (long)m * P.ldc + n, g[i]);
+      st4g(LN.dx + (long)m * LG_BN + n, d);
       pg += g[i] * xh[i];
       pbsum += g[i];
     }
@@ -1733,7 +1749,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   const float sum = (((rr[0] + rr[LG_BN]) + (rr[2 * LG_BN] + rr[3 * LG_BN])) +
                      ((rr[4 * LG_BN] + rr[5 * LG_BN]) + (rr[6 * LG_BN] + rr[7 * LG_BN])));
   const long nblk = (P.M + LB_BM - 1) / LB_BM;
-  LN.partial[(which * nblk + bx) * LG_BN + c] = sum;
+  st1g(LN.partial + (which * nblk + bx) * LG_BN + c, sum);
   if (!chain) return;
 
   // chained GEMM: dout[32 x 256 npass] = dx_tile[32 x 256] Wo[256 x 256 npass]; A from the
@@ -1745,8 +1761,22 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
   const int nsl = 8 * npass;
+  // as in gemm_ln_kernel: this wave's epilogue stores stay in flight across the slice waits —
+  // at u = 0 the 8 row stores (g, dx of 4 rows), the partial-row store and slice 1's 4 pieces
+  // are younger than slice 0; after a pass's element-form stores (16) the next slice is older
+  // than them.  Exact for full tiles; a partial tile waits for everything.
+  const bool full = m0 + LB_BM <= P.M;
   for (int u = 0; u < nsl; ++u) {
-    gl_wait_vm<0>();
+    if (!full) {
+      gl_wait_vm<0>();
+    } else if (u == 0) {
+      if (nsl > 1) gl_wait_vm<13>();
+      else gl_wait_vm<9>();
+    } else if ((u & 7) == 0) {
+      gl_wait_vm<16>();
+    } else {
+      gl_wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
@@ -1772,7 +1802,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
         if (m >= P.M) continue;
         float o = acc2[r];
         if (dgelu) o *= gelu_erf_grad(LN.aux[(long)m * ldw + cn]);
-        LN.dout[(long)m * ldw + cn] = o;
+        st1g(LN.dout + (long)m * ldw + cn, o);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
