@@ -450,9 +450,12 @@ def _ln_bwd_or_handoff(dys, vs, gam, means, rstds, lnsaved, bet):
     db = [param_grad_empty(b) for b in bet]
     part = [h[3] for h in hs]
 
+    # raw pointers, not the tensors: a closure holding dg / db would make autograd's
+    # AccumulateGrad copy them (use count > 1) instead of taking them over
+    pairs = _ptr_pairs([(part[g], dg[g]) for g in range(G)] + [(part[g], db[g], nblk * N) for g in range(G)])
+
     def reduce():
-        reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
-                    [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0)
+        reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
     finish = (reduce, part, params)
     if not _LN_AFFINE_SIDE:
         reduce()
@@ -495,13 +498,29 @@ def _ln_bwd(dys, x, gam, means, rstds, defer_affine=False, params=None):
         L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, rows, 0, 0, L.stream_handle()),
                 "sca_layernorm_bwd")
     finish = None
-    if defer_affine:
-        finish = (lambda: reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
-                                      [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0),
-                  part, params or ())
+    if defer_affine:  # pointers only: see _ln_bwd_or_handoff
+        pairs = _ptr_pairs([(part[g], dg[g]) for g in range(G)] + [(part[g], db[g], nblk * N) for g in range(G)])
+        finish = (lambda: reduce_rows_ptr(pairs, nblk, 1, N, N, 0), part, params or ())
     else:
         params_produced(params or ())
     return dx, dg, db, finish
+
+
+def _ptr_pairs(items):
+    """[(input tensor, output tensor[, input float offset])] -> [(in ptr, out ptr, 1.0)]."""
+    return [(a.data_ptr() + 4 * (it[2] if len(it) > 2 else 0), it[1].data_ptr(), 1.0) for it in items
+            for a in (it[0],)]
+
+
+def reduce_rows_ptr(pairs, S, I, N, stride_s, stride_i, accumulate=False):
+    """reduce_rows over raw device pointers [(in, out, scale)] (no tensor references kept)."""
+    lib = L.lib()
+    st = L.stream_handle()
+    for i in range(0, len(pairs), L.REDUCE_MAX_PROBLEMS):
+        chunk = pairs[i:i + L.REDUCE_MAX_PROBLEMS]
+        arr = (L.ReduceProblem * len(chunk))(*[L.ReduceProblem(a, o, s) for a, o, s in chunk])
+        L.check(lib.sca_reduce_rows(len(chunk), arr, S, I, N, stride_s, stride_i, int(accumulate), st),
+                "sca_reduce_rows")
 
 
 def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
