@@ -1314,6 +1314,17 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   const sca_gemm_ln_problem& LN = args.ln[pid];
   const int m0 = bx * BM;
   if (m0 >= P.M) return;
+#ifdef SCA_GEMM_STAMPS
+  // diagnostic build: entry, main loop done, LayerNorm done, first chained pass done, end
+  const unsigned stamp_id = wgid;
+#define SCA_LN_STAMP(slot) \
+  if (threadIdx.x == 0 && stamp_id < STAMP_MAX) g_stamps[stamp_id][slot] = __builtin_amdgcn_s_memrealtime()
+#else
+#define SCA_LN_STAMP(slot) \
+  do {                     \
+  } while (0)
+#endif
+  SCA_LN_STAMP(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const sca_gemm_seg& G = P.seg[0];
   const int total = G.K / GL_BK;
@@ -1380,6 +1391,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     }
     // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
     __syncthreads();
+    SCA_LN_STAMP(1);
     const int col = lane & 31, rowh = 4 * (lane >> 5);
 #pragma unroll
     for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
@@ -1508,6 +1520,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
     __syncthreads();  // every wave's y rows written to the image
+    SCA_LN_STAMP(2);
     // the waits for a slice's DMA let this wave's epilogue stores stay in flight (vmcnt counts
     // stores too, in issue order): at u = 0 the 16 LayerNorm stores (v, y, mean, rstd of 4
     // rows) and slice 1's 4 pieces are younger than slice 0; after a pass's epilogue its 4
@@ -1547,9 +1560,16 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
         chain_rows(LN.pass[pass_of(u)], rows, m0, P.M, 32 * wave, lane);
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+        if (u == 7) SCA_LN_STAMP(3);
       }
     }
   }
+#ifdef SCA_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  SCA_LN_STAMP(4);
+#undef SCA_LN_STAMP
 }
 
 // ------------------------------------------------------------------------------ GEMM + LayerNorm backward
