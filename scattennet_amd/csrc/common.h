@@ -42,6 +42,17 @@ typedef __attribute__((address_space(1))) float g_float;
 __device__ __forceinline__ void st4g(float* p, f32x4 v) { *(g_f32x4*)(p) = v; }
 __device__ __forceinline__ void st1g(float* p, float v) { *(g_float*)(p) = v; }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt(0))
+// but not for its global stores / loads / LDS-DMA in flight — __syncthreads() waits for those
+// too (vmcnt(0)), which would drain an epilogue's stores and the next phase's prefetched
+// slices at every such barrier.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt, expcnt unconstrained
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -1357,6 +1357,12 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     const int m = min(m0 + RPW * wave + i, P.M - 1);
     rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
   }
+  // ... and the LayerNorm's affine / the bias (complete by the end of the main loop, where a
+  // wait says so to the waitcnt pass: loaded after it, they were waited for behind the
+  // chained passes' first two slices — vmcnt(0) on 64 KB per workgroup, ~3 us)
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
+  const f32x4 gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = G.alpha;
   if constexpr (BM == 32) {
@@ -1429,12 +1435,10 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       for (int r = 0; r < 4; ++r) V[(4 * grp + r) * LG_VS + 64 * wave + 16 * j + li] = acc[j][r] * alpha;
   }
   __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every load of this wave so far has landed
 
   // each wave normalises BM/NW rows at once: every row is 64 lanes x float4 (coalesced), and
   // the rows' reductions are interleaved (independent shuffle chains, one latency each)
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
-  const f32x4 gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
   DropMask dm;
   const bool drop = (P.epi & SCA_EPI_DROPOUT) != 0;
   if (drop) dm.init(P.drop_seed, P.drop_p, args.drop_off);
@@ -1519,7 +1523,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     f32x16 acc2;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
-    __syncthreads();  // every wave's y rows written to the image
+    lds_barrier();  // every wave's y rows written to the image (its global stores stay in flight)
     SCA_LN_STAMP(2);
     // the waits for a slice's DMA let this wave's epilogue stores stay in flight (vmcnt counts
     // stores too, in issue order): at u = 0 the 16 LayerNorm stores (v, y, mean, rstd of 4
@@ -1657,6 +1661,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   const int n = 4 * lane;
   f32x4 xin[RPW], rin[RPW];
   float mu[RPW], rs[RPW];
+  const f32x4 gam = ld4(LN.gamma + n);  // the LayerNorm's gamma, with the other epilogue operands
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int m = min(m0 + RPW * wave + i, P.M - 1);
@@ -1707,7 +1712,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
   __syncthreads();
 
-  const f32x4 gam = ld4(LN.gamma + n);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed (see gemm_ln_kernel)
   const float invN = 1.0f / LG_BN;
   f32x4 g[RPW], xh[RPW];
   float s1[RPW], s2[RPW];
@@ -1763,7 +1768,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   float* red = reinterpret_cast<float*>(smem + LB_RED_OFF);
   st4(red + wave * LG_BN + n, pg);
   st4(red + (8 + wave) * LG_BN + n, pbsum);
-  __syncthreads();
+  lds_barrier();  // the partial rows are in LDS (the row stores above stay in flight)
   const int c = threadIdx.x & (LG_BN - 1), which = threadIdx.x >> 8;
   const float* rr = red + which * 8 * LG_BN + c;
   const float sum = (((rr[0] + rr[LG_BN]) + (rr[2 * LG_BN] + rr[3 * LG_BN])) +
