@@ -1298,11 +1298,17 @@ __device__ __forceinline__ void chain_rows(const sca_gemm_chain_pass& Q, const f
   }
 }
 
-template <int BM, bool CH>
+// NC = 2: d_model = 512 as two 256-column halves of one continuous slice sequence (the A
+// tile is re-read from L2 once; two accumulators per wave), one 32 x 512 epilogue tile and
+// LayerNorm over the full row; no chained passes.
+template <int BM, bool CH, int NC>
 __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmLnArgs args) {
   using CF = LgCfg<BM>;
   constexpr int S = CF::S;
+  constexpr int VS = NC * LG_BN + 8;  // row stride of the epilogue tile
+  constexpr int NROW = NC * LG_BN;
   static_assert(!CH || (BM == 32 && LG_CH_SMEM >= S * CF::STAGE && 32 * LG_VS * 4 <= LG_A2_OFF), "LDS map");
+  static_assert(NC == 1 || (NC == 2 && BM == 32 && !CH && 32 * VS * 4 <= S * CF::STAGE), "LDS map (NC = 2)");
   __shared__ __attribute__((aligned(1024))) char smem[CH ? LG_CH_SMEM : S * CF::STAGE];
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
@@ -1328,6 +1334,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const sca_gemm_seg& G = P.seg[0];
   const int total = G.K / GL_BK;
+  const int ttot = NC * total;  // slices of all column halves
 
   // DMA sources: A pieces spread over the first waves, B pieces 8*wave .. 8*wave+7 (the
   // swizzle of row r is (r >> 1) & 7: pieces 2u and 2u + 1 differ in it, pieces 16 rows
@@ -1340,40 +1347,50 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   const long pstep = 16L * G.ldb;
   auto dma = [&](int t, int stage) {
     char* base = smem + stage * CF::STAGE;
-    const long kk = (long)t * GL_BK;
+    const int half = NC == 2 && t >= total ? 1 : 0;
+    const long kk = (long)(t - half * total) * GL_BK;
+    const long hoff = (long)half * LG_BN * G.ldb;  // B rows of the second column half
     if (has_a) gl_dma(pa + kk, base + wave * GL_PIECE);
 #pragma unroll
     for (int c = 0; c < BPW; ++c)
-      gl_dma(pb[c & 1] + (c >> 1) * pstep + kk, base + CF::A_BYTES + (BPW * wave + c) * GL_PIECE);
+      gl_dma(pb[c & 1] + (c >> 1) * pstep + hoff + kk, base + CF::A_BYTES + (BPW * wave + c) * GL_PIECE);
   };
 
   // the epilogue's residual rows are loaded before the main loop (their HBM reads overlap
   // it); no residual: a harmless read of gamma, unused — keeps the loads branch-free
   constexpr int RPW = BM / CF::NW;
   const int n = 4 * lane;
-  f32x4 rin[RPW];
+  f32x4 rin[RPW][NC];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int m = min(m0 + RPW * wave + i, P.M - 1);
-    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) rin[i][c] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + LG_BN * c + n);
   }
   // ... and the LayerNorm's affine / the bias (complete by the end of the main loop, where a
   // wait says so to the waitcnt pass: loaded after it, they were waited for behind the
   // chained passes' first two slices — vmcnt(0) on 64 KB per workgroup, ~3 us)
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero;
-  const f32x4 gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
+  f32x4 bias4[NC], gam[NC], bet[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    bias4[c] = P.bias ? ld4(P.bias + LG_BN * c + n) : zero;
+    gam[c] = ld4(LN.gamma + LG_BN * c + n);
+    bet[c] = ld4(LN.beta + LG_BN * c + n);
+  }
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = G.alpha;
   if constexpr (BM == 32) {
-    f32x16 acc;
+    f32x16 acc[NC];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
 #pragma unroll
     for (int i = 0; i < S - 1; ++i)
-      if (i < total) dma(i, i);
-    for (int t = 0; t < total; ++t) {
-      if (t + S - 2 < total) {
+      if (i < ttot) dma(i, i);
+    auto slice = [&](int t, f32x16& ac) {
+      if (t + S - 2 < ttot) {
         if (has_a) gl_wait_vm<(BPW + 1) * (S - 2)>();
         else gl_wait_vm<BPW * (S - 2)>();
       } else {
@@ -1381,7 +1398,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+      if (t + S - 1 < ttot) dma(t + S - 1, (t + S - 1) % S);
       const char* As = smem + (t % S) * CF::STAGE;
       const char* Bs = As + CF::A_BYTES;
       f32x4 fa[4], fb[4];
@@ -1393,14 +1410,20 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
-    }
-    // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
+        for (int j = 0; j < 4; ++j) ac = mfma32(fa[g][j], fb[g][j], ac);
+    };
+    for (int t = 0; t < total; ++t) slice(t, acc[0]);
+    if constexpr (NC == 2)
+      for (int t = total; t < ttot; ++t) slice(t, acc[1]);
+    // 32 x 256 NC tile -> LDS (the ring is free once every wave has passed its last slice)
     __syncthreads();
     SCA_LN_STAMP(1);
     const int col = lane & 31, rowh = 4 * (lane >> 5);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        V[((r & 3) + 8 * (r >> 2) + rowh) * VS + LG_BN * c + 32 * wave + col] = acc[c][r] * alpha;
   } else {
     // 16 rows: wave w owns columns 64w .. 64w+63 as four 16x16 accumulators; per 16-k group
     // c a lane reads 4 consecutive k of its A row and of each B row (one float4 each)
@@ -1432,7 +1455,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) V[(4 * grp + r) * LG_VS + 64 * wave + 16 * j + li] = acc[j][r] * alpha;
+      for (int r = 0; r < 4; ++r) V[(4 * grp + r) * VS + 64 * wave + 16 * j + li] = acc[j][r] * alpha;
   }
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every load of this wave so far has landed
@@ -1442,19 +1465,25 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   DropMask dm;
   const bool drop = (P.epi & SCA_EPI_DROPOUT) != 0;
   if (drop) dm.init(P.drop_seed, P.drop_p, args.drop_off);
-  const float invN = 1.0f / LG_BN;
-  f32x4 v[RPW];
+  const float invN = 1.0f / NROW;
+  f32x4 v[RPW][NC];
   float s[RPW];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int lr = RPW * wave + i, m = min(m0 + lr, P.M - 1);
-    v[i] = (ld4(&V[lr * LG_VS + n]) + bias4) * P.post_scale;
-    if (drop) {
+    s[i] = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[i][j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), v[i][j]);
+    for (int c = 0; c < NC; ++c) {
+      f32x4 x = (ld4(&V[lr * VS + LG_BN * c + n]) + bias4[c]) * P.post_scale;
+      if (drop) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(LG_BN * c + n + j), x[j]);
+      }
+      if (P.resid) x += rin[i][c];
+      v[i][c] = x;
+      s[i] += (x[0] + x[1]) + (x[2] + x[3]);
     }
-    if (P.resid) v[i] += rin[i];
-    s[i] = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   }
   // chained passes: a slice of B (row r of the [256][32] image at r * 128 B, pieces 4w .. 4w+3
   // by wave w) — the first two stream in under the LayerNorm math, into the V tile's region
@@ -1489,8 +1518,12 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   float q[RPW];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const f32x4 dv = v[i] - s[i] * invN;
-    q[i] = (dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]);
+    q[i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const f32x4 dv = v[i][c] - s[i] * invN;
+      q[i] += (dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
@@ -1501,11 +1534,16 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
     const int lr = RPW * wave + i, m = m0 + lr;
     const float mean = s[i] * invN;
     const float rstd = 1.0f / sqrtf(q[i] * invN + args.eps);
-    const f32x4 y = (v[i] - mean) * rstd * gam + bet;
-    if (CH) st4(reinterpret_cast<float*>(smem + LG_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const f32x4 y = (v[i][c] - mean) * rstd * gam[c] + bet[c];
+      if (CH) st4(reinterpret_cast<float*>(smem + LG_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
+      if (m < P.M) {
+        st4g(P.C + (long)m * P.ldc + LG_BN * c + n, v[i][c]);
+        st4g(LN.y + (long)m * NROW + LG_BN * c + n, y);
+      }
+    }
     if (m < P.M) {
-      st4g(P.C + (long)m * P.ldc + n, v[i]);
-      st4g(LN.y + (long)m * LG_BN + n, y);
       if (lane == 0) {
         st1g(LN.mean + m, mean);
         st1g(LN.rstd + m, rstd);
@@ -1609,9 +1647,15 @@ struct GemmLnbArgs {
   sca_gemm_lnb_problem ln[SCA_GEMM_MAX_PROBLEMS];
 };
 
+// NC = 2: d_model = 512 as two 256-column halves (one continuous slice sequence, two
+// accumulators per wave), a 32 x 512 epilogue tile, no chained GEMM.
+template <int NC>
 __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   __shared__ __attribute__((aligned(1024))) char smem[LB_SMEM];
+  constexpr int VS = NC * LG_BN + 8, NROW = NC * LG_BN;
+  constexpr int RED_OFF = NC == 1 ? LB_RED_OFF : LB_BM * VS * 4;  // dgamma / dbeta wave partials
   static_assert(LB_B2 >= LB_BM * LG_VS * 4 && LB_RED_OFF + 2 * 8 * LG_BN * 4 <= LB_SMEM, "LDS map");
+  static_assert(NC == 1 || RED_OFF + 2 * 8 * NROW * 4 <= LB_SMEM, "LDS map (NC = 2)");
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
   const unsigned orig = blockIdx.x + gx * blockIdx.z;
@@ -1632,12 +1676,19 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     seg_n[s] = s < P.nseg ? P.seg[s].K / GL_BK : 0;
     total += seg_n[s];
   }
+  const int ttot = NC * total;  // slices of all column halves
   // issue state: A piece `wave` (rows 8*wave ..) and B pieces = k-rows 4*wave .. 4*wave+3
   int iseg = -1, tseg0 = 0, tend = 0;
   const float* pa = nullptr;
   const float* pb = nullptr;
   long ldb = 0;
   auto dma = [&](int t, int stage) {
+    const int half = NC == 2 && t >= total ? 1 : 0;
+    if (NC == 2 && t == total) {  // second column half: the segments again
+      iseg = -1;
+      tend = 0;
+    }
+    t -= half * total;
     while (t >= tend) {
       ++iseg;
       tseg0 = tend;
@@ -1645,7 +1696,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
       const sca_gemm_seg& G = P.seg[iseg];
       pa = lg_src(G.A, G.lda, m0, P.M, has_a ? wave : 0, lane);
       ldb = G.ldb;
-      pb = G.B + (long)(4 * wave) * ldb + 4 * lane;
+      pb = G.B + (long)(4 * wave) * ldb + 4 * lane + LG_BN * half;
     }
     const long k0 = (long)(t - tseg0) * GL_BK;
     char* base = smem + stage * LB_STAGE;
@@ -1659,28 +1710,35 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   // instead of forming the HBM-bound tail of every workgroup at once
   constexpr int RPW = LB_BM / 8;
   const int n = 4 * lane;
-  f32x4 xin[RPW], rin[RPW];
+  f32x4 xin[RPW][NC], rin[RPW][NC], gam[NC];
   float mu[RPW], rs[RPW];
-  const f32x4 gam = ld4(LN.gamma + n);  // the LayerNorm's gamma, with the other epilogue operands
+#pragma unroll
+  for (int c = 0; c < NC; ++c) gam[c] = ld4(LN.gamma + LG_BN * c + n);  // with the other epilogue operands
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int m = min(m0 + RPW * wave + i, P.M - 1);
-    xin[i] = ld4(LN.x + (long)m * LG_BN + n);
-    if (LN.tab) xin[i] += ld4(LN.tab + (long)(m % LN.tab_T + 2) * LG_BN + n);  // v = x + P[t + 2]
-    // (no residual: a harmless read of gamma, unused — keeps the loads branch-free)
-    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int nc = LG_BN * c + n;
+      xin[i][c] = ld4(LN.x + (long)m * NROW + nc);
+      if (LN.tab) xin[i][c] += ld4(LN.tab + (long)(m % LN.tab_T + 2) * NROW + nc);  // v = x + P[t + 2]
+      // (no residual: a harmless read of gamma, unused — keeps the loads branch-free)
+      rin[i][c] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + nc);
+    }
     mu[i] = LN.mean[m];
     rs[i] = LN.rstd[m];
   }
-  f32x16 acc;
+  f32x16 acc[NC];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
   const int col = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int i = 0; i < LB_S - 1; ++i)
-    if (i < total) dma(i, i);
-  for (int t = 0; t < total; ++t) {
-    if (t + LB_S - 2 < total) {
+    if (i < ttot) dma(i, i);
+  auto slice = [&](int t, f32x16& ac) {
+    if (t + LB_S - 2 < ttot) {
       if (has_a) gl_wait_vm<5 * (LB_S - 2)>();
       else gl_wait_vm<4 * (LB_S - 2)>();
     } else {
@@ -1688,7 +1746,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + LB_S - 1 < total) dma(t + LB_S - 1, (t + LB_S - 1) % LB_S);
+    if (t + LB_S - 1 < ttot) dma(t + LB_S - 1, (t + LB_S - 1) % LB_S);
     const char* As = smem + (t % LB_S) * LB_STAGE;
     const float* Bf = reinterpret_cast<const float*>(As + LB_A_BYTES);
     f32x4 fa[4], fb[4];
@@ -1701,35 +1759,45 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
-  }
-  // 32x256 tile -> LDS (the ring is free once every wave has passed its last slice)
+      for (int j = 0; j < 4; ++j) ac = mfma32(fa[g][j], fb[g][j], ac);
+  };
+  for (int t = 0; t < total; ++t) slice(t, acc[0]);
+  if constexpr (NC == 2)
+    for (int t = total; t < ttot; ++t) slice(t, acc[1]);
+  // 32 x 256 NC tile -> LDS (the ring is free once every wave has passed its last slice)
   __syncthreads();
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = P.seg[0].alpha;
   const int rowh = 4 * h;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) V[((r & 3) + 8 * (r >> 2) + rowh) * LG_VS + 32 * wave + col] = acc[r] * alpha;
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      V[((r & 3) + 8 * (r >> 2) + rowh) * VS + LG_BN * c + 32 * wave + col] = acc[c][r] * alpha;
   __syncthreads();
 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed (see gemm_ln_kernel)
-  const float invN = 1.0f / LG_BN;
-  f32x4 g[RPW], xh[RPW];
+  const float invN = 1.0f / NROW;
+  f32x4 g[RPW][NC], xh[RPW][NC];
   float s1[RPW], s2[RPW];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    g[i] = ld4(&V[(RPW * wave + i) * LG_VS + n]);
-    if (P.resid) g[i] += rin[i];
-    xh[i] = (xin[i] - mu[i]) * rs[i];
-    const f32x4 gg = g[i] * gam;
-    s1[i] = (gg[0] + gg[1]) + (gg[2] + gg[3]);
-    const f32x4 ggx = gg * xh[i];
-    s2[i] = (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
+    s1[i] = s2[i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      g[i][c] = ld4(&V[(RPW * wave + i) * VS + LG_BN * c + n]);
+      if (P.resid) g[i][c] += rin[i][c];
+      xh[i][c] = (xin[i][c] - mu[i]) * rs[i];
+      const f32x4 gg = g[i][c] * gam[c];
+      s1[i] += (gg[0] + gg[1]) + (gg[2] + gg[3]);
+      const f32x4 ggx = gg * xh[i][c];
+      s2[i] += (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
+    }
   }
   // chained GEMM (dout = dx Wo, npass 256-column blocks of Wo): its first two B slices
   // stream in under the LayerNorm math, into the V tile's region once every wave has read
   // its rows of it; the passes are one continuous slice sequence
-  const bool chain = LN.wo != nullptr;
+  const bool chain = NC == 1 && LN.wo != nullptr;
   const int npass = chain ? max(LN.npass, 1) : 0;
   const long ldw = LN.ldw ? LN.ldw : (long)LG_BN * npass;
   const float* pw = LN.wo + (long)(4 * wave) * ldw + 4 * lane;  // B pieces: k-rows 4*wave .. +3
@@ -1750,31 +1818,44 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
       s1[i] += __shfl_xor(s1[i], o, 64);
       s2[i] += __shfl_xor(s2[i], o, 64);
     }
-  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pbsum = {0.f, 0.f, 0.f, 0.f};
+  f32x4 pg[NC], pbsum[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) pg[c] = pbsum[c] = f32x4{0.f, 0.f, 0.f, 0.f};
   float* A2 = reinterpret_cast<float*>(smem + LB_A2_OFF);
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
     const int lr = RPW * wave + i, m = m0 + lr;
-    const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rs[i];
-    if (chain) st4(A2 + lr * LB_A2_LD + n, d);  // rows past M: finite, their products never stored
-    if (m < P.M) {
-      st4g(P.C + (long)m * P.ldc + n, g[i]);
-      st4g(LN.dx + (long)m * LG_BN + n, d);
-      pg += g[i] * xh[i];
-      pbsum += g[i];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const f32x4 d = (g[i][c] * gam[c] - s1[i] * invN - xh[i][c] * (s2[i] * invN)) * rs[i];
+      if (chain) st4(A2 + lr * LB_A2_LD + n, d);  // rows past M: finite, their products never stored
+      if (m < P.M) {
+        st4g(P.C + (long)m * P.ldc + LG_BN * c + n, g[i][c]);
+        st4g(LN.dx + (long)m * NROW + LG_BN * c + n, d);
+        pg[c] += g[i][c] * xh[i][c];
+        pbsum[c] += g[i][c];
+      }
     }
   }
-  // the 8 waves' partial rows, summed in fixed order: threads 0-255 dgamma, 256-511 dbeta
-  float* red = reinterpret_cast<float*>(smem + LB_RED_OFF);
-  st4(red + wave * LG_BN + n, pg);
-  st4(red + (8 + wave) * LG_BN + n, pbsum);
+  // the 8 waves' partial rows, summed in fixed order: dgamma, then dbeta (a thread per
+  // column, NC columns per thread)
+  float* red = reinterpret_cast<float*>(smem + RED_OFF);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    st4(red + wave * NROW + LG_BN * c + n, pg[c]);
+    st4(red + (8 + wave) * NROW + LG_BN * c + n, pbsum[c]);
+  }
   lds_barrier();  // the partial rows are in LDS (the row stores above stay in flight)
-  const int c = threadIdx.x & (LG_BN - 1), which = threadIdx.x >> 8;
-  const float* rr = red + which * 8 * LG_BN + c;
-  const float sum = (((rr[0] + rr[LG_BN]) + (rr[2 * LG_BN] + rr[3 * LG_BN])) +
-                     ((rr[4 * LG_BN] + rr[5 * LG_BN]) + (rr[6 * LG_BN] + rr[7 * LG_BN])));
   const long nblk = (P.M + LB_BM - 1) / LB_BM;
-  st1g(LN.partial + (which * nblk + bx) * LG_BN + c, sum);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e = threadIdx.x + 512 * c;  // (which, column) of 2 x NROW sums
+    const int cc = e % NROW, which = e / NROW;
+    const float* rr = red + which * 8 * NROW + cc;
+    const float sum = (((rr[0] + rr[NROW]) + (rr[2 * NROW] + rr[3 * NROW])) +
+                       ((rr[4 * NROW] + rr[5 * NROW]) + (rr[6 * NROW] + rr[7 * NROW])));
+    st1g(LN.partial + (which * nblk + bx) * NROW + cc, sum);
+  }
   if (!chain) return;
 
   // chained GEMM: dout[32 x 256 npass] = dx_tile[32 x 256] Wo[256 x 256 npass]; A from the
@@ -2443,6 +2524,7 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
   a.eps = eps;
   a.drop_off = sca_drop_offset_ptr();
   int maxM = 0;
+  const int N = probs[0].N;  // 256, or 512 (two column halves, no chained passes)
   for (int i = 0; i < nprob; ++i) {
     const sca_gemm_problem& P = probs[i];
     const sca_gemm_ln_problem& L = ln[i];
@@ -2451,16 +2533,17 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
                          reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
                          reinterpret_cast<uintptr_t>(P.bias) | reinterpret_cast<uintptr_t>(L.y) |
                          reinterpret_cast<uintptr_t>(L.gamma) | reinterpret_cast<uintptr_t>(L.beta)) & 15);
-    if (P.nseg != 1 || P.N != LG_BN || P.M < 0 || S.K < GL_BK || (S.K % GL_BK) || !S.A || !S.B || !P.C ||
-        !L.gamma || !L.beta || !L.y || !L.mean || !L.rstd || !al16 || (S.lda & 3) || (S.ldb & 3) ||
-        S.lda < S.K || S.ldb < S.K || (P.ldc & 3) || P.ldc < LG_BN || (P.resid && ((P.ldr & 3) || P.ldr < LG_BN)) ||
+    if (P.nseg != 1 || (N != LG_BN && N != 2 * LG_BN) || P.N != N || P.M < 0 || S.K < GL_BK || (S.K % GL_BK) ||
+        !S.A || !S.B || !P.C || !L.gamma || !L.beta || !L.y || !L.mean || !L.rstd || !al16 || (S.lda & 3) ||
+        (S.ldb & 3) || S.lda < S.K || S.ldb < S.K || (P.ldc & 3) || P.ldc < N || (P.resid && ((P.ldr & 3) || P.ldr < N)) ||
         (P.epi & ~SCA_EPI_DROPOUT) || ((P.epi & SCA_EPI_DROPOUT) && !(P.drop_p >= 0.f && P.drop_p < 1.f))) {
-      sca_set_error("sca_gemm_ln: needs one segment, N == 256, K a positive multiple of 32, 16-byte aligned "
-                    "operands with leading dimensions multiple of 4, and no epilogue other than dropout");
+      sca_set_error("sca_gemm_ln: needs one segment, N == 256 or 512 (the same for every problem), K a positive "
+                    "multiple of 32, 16-byte aligned operands with leading dimensions multiple of 4, and no "
+                    "epilogue other than dropout");
       return SCA_ERR_ARG;
     }
-    if (L.npass < 0 || L.npass > 3) {
-      sca_set_error("sca_gemm_ln: npass must be 0..3");
+    if (L.npass < 0 || L.npass > 3 || (N != LG_BN && L.npass != 0)) {
+      sca_set_error("sca_gemm_ln: npass must be 0..3 (0 at N = 512)");
       return SCA_ERR_ARG;
     }
     for (int q = 0; q < L.npass; ++q) {
@@ -2483,12 +2566,14 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
   if (maxM == 0) return SCA_OK;
   const int bm = sca_gemm_ln_rows(nprob, maxM, chain);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (chain) {
-    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+  if (N != LG_BN) {
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 2>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+  } else if (chain) {
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true, 1>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   } else if (bm == 16) {
-    hipLaunchKernelGGL((gemm_ln_kernel<GL_A16, false>), dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A16, false, 1>), dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 1>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
@@ -2505,13 +2590,15 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
   }
   GemmLnbArgs a;
   int maxM = 0;
+  const int N = probs[0].N;  // 256, or 512 (two column halves, no chained GEMM)
   for (int i = 0; i < nprob; ++i) {
     const sca_gemm_problem& P = probs[i];
     const sca_gemm_lnb_problem& L = lnb[i];
-    bool ok = P.nseg >= 1 && P.nseg <= SCA_GEMM_MAX_SEGS && P.N == LG_BN && P.M >= 0 && P.C && L.x && L.mean &&
+    bool ok = P.nseg >= 1 && P.nseg <= SCA_GEMM_MAX_SEGS && (N == LG_BN || N == 2 * LG_BN) && P.N == N &&
+              P.M >= 0 && P.C && L.x && L.mean &&
               L.rstd && L.gamma && L.dx && L.partial && P.epi == 0 && !P.bias && !P.bias_grad &&
-              P.post_scale == 1.f && (P.ldc & 3) == 0 && P.ldc >= LG_BN &&
-              (!P.resid || ((P.ldr & 3) == 0 && P.ldr >= LG_BN)) &&
+              P.post_scale == 1.f && (P.ldc & 3) == 0 && P.ldc >= N &&
+              (!P.resid || ((P.ldr & 3) == 0 && P.ldr >= N)) && (N == LG_BN || !L.wo) &&
               (!L.tab || (L.tab_T >= 1 && !(reinterpret_cast<uintptr_t>(L.tab) & 15)));
     uintptr_t al = reinterpret_cast<uintptr_t>(P.C) | reinterpret_cast<uintptr_t>(P.resid) |
                    reinterpret_cast<uintptr_t>(L.x) | reinterpret_cast<uintptr_t>(L.gamma) |
@@ -2526,13 +2613,14 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
     for (int s = 0; ok && s < P.nseg; ++s) {
       const sca_gemm_seg& S = P.seg[s];
       ok = S.A && S.B && S.K >= GL_BK && S.K % GL_BK == 0 && (S.lda & 3) == 0 && S.lda >= S.K &&
-           (S.ldb & 3) == 0 && S.ldb >= LG_BN && S.alpha == P.seg[0].alpha;
+           (S.ldb & 3) == 0 && S.ldb >= N && S.alpha == P.seg[0].alpha;
       al |= reinterpret_cast<uintptr_t>(S.A) | reinterpret_cast<uintptr_t>(S.B);
     }
     if (!ok || (al & 15)) {
-      sca_set_error("sca_gemm_lnb: needs N == 256, 1-3 segments with K a positive multiple of 32 and one alpha, "
-                    "k-major B, no epilogue other than resid, 16-byte aligned operands with leading dimensions "
-                    "multiple of 4; chained: wo and dout both or neither, npass 0..3, ldw >= 256 npass");
+      sca_set_error("sca_gemm_lnb: needs N == 256 or 512 (the same for every problem), 1-3 segments with K a "
+                    "positive multiple of 32 and one alpha, k-major B, no epilogue other than resid, 16-byte aligned "
+                    "operands with leading dimensions multiple of 4; chained (N == 256 only): wo and dout both or "
+                    "neither, npass 0..3, ldw >= 256 npass");
       return SCA_ERR_ARG;
     }
     a.p[i] = P;
@@ -2541,7 +2629,8 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
   }
   if (maxM == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(gemm_lnb_kernel, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  if (N == LG_BN) hipLaunchKernelGGL(gemm_lnb_kernel<1>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(gemm_lnb_kernel<2>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

@@ -227,8 +227,22 @@ _LN_AFFINE_SIDE = __import__("os").environ.get("SCA_LN_AFFINE_SIDE", "1") != "0"
 _FUSE_LN = __import__("os").environ.get("SCA_FUSE_LN", "1") != "0"
 
 
+# d_model 512 (two 256-column halves, no chained passes): parity-green, but slower than the
+# plain 64x64-tile GEMMs + separate LayerNorm launches at config 5 (71.9 vs 70.6 ms/step:
+# the 32-row x 256-column tiles at one workgroup per CU run the big-M GEMMs at ~0.43 of
+# peak against the plain kernel's ~0.6, which outweighs the LayerNorm launches saved;
+# tools/r03_t13.sh / r03_t14.sh) — opt-in (SCA_FUSE_LN512=1)
+_FUSE_LN512 = __import__("os").environ.get("SCA_FUSE_LN512", "0") != "0"
+
+
+def ln_width_ok(N):
+    """LayerNorm widths the fused GEMM + LayerNorm launches take (forward and backward)."""
+    return N == 256 or (N == 512 and _FUSE_LN512)
+
+
 def ln_fusable(N, K):
-    return _FUSE_LN and N == 256 and K >= 32 and K % 32 == 0
+    """d_model 256 (chained passes possible) or, opt-in, 512 (two column halves)."""
+    return _FUSE_LN and ln_width_ok(N) and K >= 32 and K % 32 == 0
 
 
 def gemm_ln(probs, lns, eps):
@@ -243,8 +257,9 @@ def gemm_ln(probs, lns, eps):
             if _PROFILER else 0.0
         # the variant sca_gemm_ln picks, for the kernel name rocprofv3 shows
         chain = any(ln.npass > 0 for ln in lchunk)
-        bm = lib.sca_gemm_ln_rows(len(chunk), max(p.M for p in chunk), int(chain))
-        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}>", flops):
+        nc = chunk[0].N // 256
+        bm = 32 if nc > 1 else lib.sca_gemm_ln_rows(len(chunk), max(p.M for p in chunk), int(chain))
+        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}>", flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
@@ -378,8 +393,8 @@ _CHAIN_MIN_TILES = int(__import__("os").environ.get("SCA_CHAIN_MIN_TILES", "256"
 
 def _chain_lns(nxt, G, M, like, gam, bet, ys, means, rstds):
     """GemmLnProblems of a fused GEMM + LayerNorm launch, with `nxt`'s chained passes."""
-    if nxt is not None and G * ((M + 31) // 32) < _CHAIN_MIN_TILES:
-        nxt = None
+    if nxt is not None and (G * ((M + 31) // 32) < _CHAIN_MIN_TILES or like.shape[-1] != 256):
+        nxt = None  # (chained passes exist for d_model 256 only)
     lns = []
     for g in range(G):
         ps = nxt.passes(g, M, like) if nxt is not None else []
@@ -399,7 +414,9 @@ def gemm_lnb(probs, lnp):
     dv = [torch.empty_like(o.v) for o in lnp]
     part = [o.v.new_empty(2 * nblk * o.v.shape[-1]) for o in lnp]
     # the producers' next GEMM on dv (dO = dv Wo, or dz = (dv W2) gelu'(z)) in the same launch
-    chain = all(o.wo is not None for o in lnp) and len({(o.wo.shape[1], o.aux is None) for o in lnp}) == 1
+    # (d_model 256 only)
+    chain = (probs[0].N == 256 and all(o.wo is not None for o in lnp) and
+             len({(o.wo.shape[1], o.aux is None) for o in lnp}) == 1)
     n2 = lnp[0].wo.shape[1] if chain else 0
     dout = [o.v.new_empty(*o.v.shape[:-1], n2) for o in lnp] if chain else [None] * len(lnp)
     arr = (L.GemmProblem * len(probs))(*probs)
@@ -412,7 +429,7 @@ def gemm_lnb(probs, lnp):
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
-    with _timed("gemm_lnb_kernel", flops):
+    with _timed(f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
 
@@ -1083,7 +1100,7 @@ class AttentionBlock(Function):
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
         ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, Wo if drop_p == 0 else None) if ln else None
-        ctx.lnprev = lnprev if (lnprev is not None and d == 256 and has_resid) else None
+        ctx.lnprev = lnprev if (lnprev is not None and ln_width_ok(d) and has_resid) else None
         ctx.save_for_backward(key_valid, add_mask, *xq, *(xkv if cross else []), *W, *Wo, *bo, *q, *k, *v, *o,
                               *sm, *sl, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
@@ -1280,7 +1297,7 @@ class FeedForwardResidual(Function):
         dz_chain = drop_p == 0 and _CHAIN_DZ
         ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, W2 if dz_chain else None,
                                        zs if dz_chain else None) if ln else None
-        ctx.lnprev = lnprev if (lnprev is not None and d == 256 and has_r and F_ % 32 == 0) else None
+        ctx.lnprev = lnprev if (lnprev is not None and ln_width_ok(d) and has_r and F_ % 32 == 0) else None
         ctx.save_for_backward(*x, *W1, *W2, *zs, *acts, *((*vs, *gam, *means, *rstds) if ln else ()))
         return tuple(ys)
 
@@ -1379,7 +1396,7 @@ class LayerNormAdd(Function):
         # the embedding LayerNorm (position table, no tail, no dropout): its backward can ride
         # in the consuming attention block's input-gradient GEMM (sca_gemm_lnb, tab mode)
         ctx.lnsaved = None
-        if pos_table and not has_post and not act and drop_p == 0 and N == 256 and _FUSE_LNB and _EMB_LNB:
+        if pos_table and not has_post and not act and drop_p == 0 and ln_width_ok(N) and _FUSE_LNB and _EMB_LNB:
             ctx.lnsaved = [LnSaved(x[g], means[g], rstds[g], gam[g], tab=tab[g], T=T) for g in range(G)]
             for y, o in zip(ys, ctx.lnsaved):
                 y._sca_ln = o

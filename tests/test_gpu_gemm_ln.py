@@ -22,13 +22,15 @@ def _need_gpu():
         pytest.skip("needs a GPU")
 
 
-@pytest.mark.parametrize("M,K", [(8192, 256), (2048, 768), (100, 64), (33, 32)])
-def test_gemm_ln_c_abi_vs_float64(M, K):
+@pytest.mark.parametrize("M,K,N", [(8192, 256, 256), (2048, 768, 256), (100, 64, 256), (33, 32, 256),
+                                   (8192, 512, 512), (2048, 2048, 512), (100, 64, 512), (33, 32, 512)])
+def test_gemm_ln_c_abi_vs_float64(M, K, N):
+    """N = 512 (cfg5's d_model): two 256-column halves of one slice sequence, one LayerNorm
+    over the 512-wide row."""
     _need_gpu()
     from scattennet_amd import _lib as L, ops
     dev = torch.device("cuda:0")
-    torch.manual_seed(M + K)
-    N = 256
+    torch.manual_seed(M + K + N)
     A, W = torch.randn(M, K, device=dev), torch.randn(N, K, device=dev) / K ** 0.5
     bias, resid = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
     gam, bet = torch.randn(N, device=dev), torch.randn(N, device=dev)

@@ -89,6 +89,65 @@ def test_gemm_lnb_c_abi_vs_float64(M, Ks, chain):
             assert torch.isnan(dout[:, n:]).all()  # columns past the passes untouched
 
 
+@pytest.mark.parametrize("tab", [False, True])
+@pytest.mark.parametrize("M,Ks", [(2048, (2048,)), (2048, (512, 512, 512)), (1000, (512,)), (33, (32, 64))])
+def test_gemm_lnb_n512_vs_float64(M, Ks, tab):
+    """d_model 512 (cfg5): two 256-column halves of one slice sequence (segments walked once
+    per half), the LayerNorm backward over the 512-wide row, dgamma / dbeta partials of 512
+    columns; `tab`: the position-table mode (LN input x + P[t + 2], the embedding LayerNorm)."""
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    torch.manual_seed(M + sum(Ks) + tab)
+    N, T = 512, 50
+    segs, c64, keep = [], torch.zeros(M, N, dtype=torch.float64), []
+    for K in Ks:
+        A, B = torch.randn(M, K, device=dev), torch.randn(K, N, device=dev) / K ** 0.5
+        keep += [A, B]
+        segs.append(ops._seg(A, B, K, N, K))
+        c64 += A.double().cpu() @ B.double().cpu()
+    resid = torch.randn(M, N, device=dev)
+    c64 += resid.double().cpu()
+    x = torch.randn(M, N, device=dev) * 2 + 0.5
+    P = torch.randn(T + 2, N, device=dev) if tab else None
+    xin = x + P[2:][torch.arange(M, device=dev) % T] if tab else x
+    gam = torch.randn(N, device=dev)
+    mean = xin.mean(-1)
+    rstd = 1.0 / (xin.var(-1, unbiased=False) + 1e-5).sqrt()
+    C, dx = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    nblk = L.lib().sca_gemm_lnb_blocks(M)
+    part = torch.empty(2 * nblk * N, device=dev)
+    prob = ops._prob(segs, C, M, N, N, resid=resid, ldr=N)
+    lnp = L.GemmLnbProblem(x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gam.data_ptr(), dx.data_ptr(),
+                           part.data_ptr(), None, None, None, 0, 0, P.data_ptr() if tab else None, T if tab else 0)
+    arr, larr = (L.GemmProblem * 1)(prob), (L.GemmLnbProblem * 1)(lnp)
+    L.check(L.lib().sca_gemm_lnb(1, arr, larr, L.stream_handle()), "sca_gemm_lnb")
+    torch.cuda.synchronize()
+    x64 = xin.double().cpu().requires_grad_(True)
+    g64, b64 = gam.double().cpu().requires_grad_(True), torch.zeros(N, dtype=torch.float64, requires_grad=True)
+    torch.nn.functional.layer_norm(x64, (N,), g64, b64, 1e-5).backward(c64)
+    assert rel_err(C.cpu(), c64) < 1e-5
+    assert rel_err(dx.cpu(), x64.grad) < 1e-4
+    assert rel_err(part[:nblk * N].view(nblk, N).sum(0).cpu(), g64.grad) < 1e-4
+    assert rel_err(part[nblk * N:].view(nblk, N).sum(0).cpu(), b64.grad) < 1e-4
+
+
+def test_gemm_lnb_n512_rejects_chain():
+    """The chained GEMM (dout = dx Wo) exists for d_model 256 only."""
+    _need_gpu()
+    from scattennet_amd import _lib as L, ops
+    dev = torch.device("cuda:0")
+    M, N = 64, 512
+    A, B, C = torch.randn(M, 64, device=dev), torch.randn(64, N, device=dev), torch.empty(M, N, device=dev)
+    prob = ops._prob([ops._seg(A, B, 64, N, 64)], C, M, N, N)
+    t = torch.empty(M, N, device=dev)
+    lnp = L.GemmLnbProblem(t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(), t.data_ptr(),
+                           t.data_ptr(), t.data_ptr(), None, 1, 0)
+    with pytest.raises(ValueError):
+        L.check(L.lib().sca_gemm_lnb(1, (L.GemmProblem * 1)(prob), (L.GemmLnbProblem * 1)(lnp),
+                                     L.stream_handle()), "sca_gemm_lnb")
+
+
 def test_gemm_lnb_rejects_bad_shapes():
     _need_gpu()
     from scattennet_amd import _lib as L, ops
@@ -141,7 +200,7 @@ def test_chained_blocks_hand_off_layer_norm_backward(second_consumer, dz, monkey
     torch.cuda.synchronize()
     # hand-offs: block 1's FFN -> its attention LN; block 1's attention -> block 0's last LN;
     # block 0's FFN -> its attention LN (block 0's attention input x has no fused producer)
-    assert prof.stats().get("gemm_lnb_kernel", {}).get("launches", 0) == 3
+    assert prof.stats().get("gemm_lnb_kernel<1>", {}).get("launches", 0) == 3
     # NN launches: block 0's attention dX (no fused producer), block 1's FFN dz (its output has
     # no fused consumer) and block 0's FFN dz unless block 1's launch chained it
     nn = prof.stats().get(ops._GEMM_NAMES[L.GEMM_NN], {}).get("launches", 0)

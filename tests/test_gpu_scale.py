@@ -52,8 +52,12 @@ def test_cfg2_four_streams_vs_oracle():
     _run("cfg2", W.WORKLOADS["cfg2"])
 
 
-def test_cfg5_long_sequence_vs_oracle():
-    # one stream of the T=1024, d=512 (hd=32) config: the causal y-stream tiles through LDS
+@pytest.mark.parametrize("fuse512", [False, True])
+def test_cfg5_long_sequence_vs_oracle(fuse512, monkeypatch):
+    # one stream of the T=1024, d=512 (hd=32) config: the causal y-stream tiles through LDS;
+    # fuse512: the post-LN LayerNorms in the GEMM launches at d_model 512 (opt-in path)
+    from scattennet_amd import ops
+    monkeypatch.setattr(ops, "_FUSE_LN512", fuse512)
     _run("cfg5", W.WORKLOADS["cfg5"], streams_used=1)
 
 
