@@ -12,7 +12,7 @@ the forward/backward run the grouped HIP kernels of `ops.py` (no ATen math on th
 import torch
 from torch import nn
 
-from . import ops
+from . import library, ops
 
 
 class BaseAttention(nn.Module):
@@ -127,7 +127,7 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
     fuse = ln is not None and ops.ln_fusable(d, d)
     if fuse:
         ts += [n.weight for n in ln] + [n.bias for n in ln]
-    out = list(ops.AttentionBlock.apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
+    out = list(library.attention_block_apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
                                         bool(resid), float(drop_p), float(ln[0].eps) if fuse else None,
                                         nxt if fuse else None, kvacc if kind == "cross" else None, attn_p, *ts))
     if ln is not None and not fuse:

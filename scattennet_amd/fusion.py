@@ -2,7 +2,7 @@
 the cross-stream fusion of the left / right / body stream encodings (BASELINE config 3)."""
 import torch.nn as nn
 
-from . import ops
+from . import library, ops
 from .layers import drop_p, layernorm_grouped
 
 
@@ -11,9 +11,7 @@ def _lin(layers, xs, gelu=False, resid=None):
     W = [l.weight for l in layers]
     b = [l.bias for l in layers]
     extra = list(resid) if resid is not None else []
-    if gelu:
-        return list(ops.LinearGelu.apply(G, resid is not None, *xs, *W, *b, *extra))
-    return list(ops.LinearResidual.apply(G, resid is not None, *xs, *W, *b, *extra))
+    return list(library.linear_apply(G, resid is not None, *xs, *W, *b, *extra, gelu=gelu))
 
 
 class CoordinatesFusion(nn.Module):
@@ -38,10 +36,10 @@ class CoordinatesFusion(nn.Module):
         p = drop_p([self], "drop_rate")
         lo, ro, bo = _lin([self.left_se, self.right_se, self.body_se], [left_embed, right_embed, body_embed],
                           gelu=True)
-        attn = ops.SoftmaxRows.apply(ops.ClipMatmul.apply(True, ro, lo))
+        attn = library.softmax_rows_apply(library.clip_matmul_apply(True, ro, lo))
         if p > 0:  # fusion.py:48
             attn = ops.dropout_grouped([attn], p)[0]
-        fuse = ops.ClipMatmul.apply(False, attn, bo)
+        fuse = library.clip_matmul_apply(False, attn, bo)
         fuse = _lin([self.out_proj], [fuse])
         fuse = layernorm_grouped([self.norm], fuse)[0]
         fuse = self.inverted_res(fuse)

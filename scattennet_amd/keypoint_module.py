@@ -8,7 +8,7 @@ the G = 1 case.  `KeypointStreams` drives several KeypointModules that way.
 import torch
 from torch import nn
 
-from . import ops
+from . import library, ops
 from .attention import CrossAttention, SelfAttention, SelfCausalAttention, attention_grouped
 from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, coordinate_mapping_grouped, drop_p,
                      fc1_request, ffn_grouped, pos_embed_layernorm_grouped)
@@ -60,7 +60,7 @@ def coordinate_attention_grouped(blocks, xs, mask, nxt=None):
 def qkv_request(blocks):
     """ops.NextProjections for the q / k / v projections of self / causal attention blocks
     (q carries the 1/sqrt(head_dim) scale, as AttentionBlock computes it)."""
-    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "fc1":
+    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "fc1" or library.compiling():
         return None
     specs = []
     for b in blocks:
@@ -142,7 +142,8 @@ def sca_grouped(scas, xs, ys, attention_mask):
     causal_mask = self_mask.causal_view()  # model/utils.py:15-28 (same key validity, +1 on j <= i)
     cross_mask = self_mask  # create_attention_mask(tgt_len=T) — same key padding
     L = len(scas[0].self_attn_layers)
-    branch = _branch_stream(se[0].device) if (L > 0 and _BRANCH_OVERLAP and se[0].is_cuda) else None
+    branch = _branch_stream(se[0].device) if (L > 0 and _BRANCH_OVERLAP and se[0].is_cuda and
+                                              not library.compiling()) else None
     s = se
     if branch is not None:
         # The self stack reads only the x stream and the first causal layer only the y stream:
@@ -162,7 +163,7 @@ def sca_grouped(scas, xs, ys, attention_mask):
     c = ce
     # the merge layers all read the final x-stream map s; their backward runs L-1 .. 0, so
     # its gradient accumulates in their GEMM epilogues instead of L-1 autograd adds
-    kvacc = ops.KvGradAccumulator() if (ops._KV_ACC and L > 1) else None
+    kvacc = ops.KvGradAccumulator() if (ops._KV_ACC and L > 1 and not library.compiling()) else None
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
         if i == 0 and branch is not None:

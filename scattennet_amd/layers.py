@@ -2,7 +2,7 @@
 import torch
 from torch import nn
 
-from . import ops
+from . import library, ops
 
 
 class LearningPositionEmbedding(nn.Embedding):
@@ -23,7 +23,7 @@ class LearningPositionEmbedding(nn.Embedding):
 
 def pos_embed_layernorm_grouped(tables, norms, xs, drop_p=0.0):
     """G-way fused  dropout(LayerNorm(x + table[2:T+2]))  (keypoint_module.py:154-165)."""
-    return list(ops.LayerNormAdd.apply(len(xs), norms[0].eps, True, False, 0, float(drop_p), *xs,
+    return list(library.layer_norm_add_apply(len(xs), norms[0].eps, True, False, 0, float(drop_p), *xs,
                                        *[e.weight for e in tables], *[n.weight for n in norms],
                                        *[n.bias for n in norms]))
 
@@ -31,7 +31,7 @@ def pos_embed_layernorm_grouped(tables, norms, xs, drop_p=0.0):
 def layernorm_grouped(norms, xs, post=None, relu=False):
     """G-way y = act(LayerNorm(x) + post)."""
     extra = list(post) if post is not None else []
-    return list(ops.LayerNormAdd.apply(len(xs), norms[0].eps, False, post is not None, 1 if relu else 0, 0.0, *xs,
+    return list(library.layer_norm_add_apply(len(xs), norms[0].eps, False, post is not None, 1 if relu else 0, 0.0, *xs,
                                        *extra, *[n.weight for n in norms], *[n.bias for n in norms]))
 
 
@@ -58,7 +58,7 @@ def ffn_grouped(ffns, xs, residual=True, ln=None, nxt=None):
     fuse = ln is not None and ops.ln_fusable(xs[0].shape[-1], ffns[0].fc2.weight.shape[1])
     if fuse:
         ts += [n.weight for n in ln] + [n.bias for n in ln]
-    out = list(ops.FeedForwardResidual.apply(G, residual, drop_p(ffns), float(ln[0].eps) if fuse else None,
+    out = list(library.feed_forward_apply(G, residual, drop_p(ffns), float(ln[0].eps) if fuse else None,
                                              nxt if fuse else None, *ts))
     if ln is not None and not fuse:
         out = layernorm_grouped(ln, out)
@@ -83,7 +83,7 @@ def fc1_request(ffns):
     """ops.NextProjections for the FFNs' fc1 (bias + GELU, keeping the pre-activation),
     computed in the launch that produces their input; None when not applicable (dropout
     inside the FFN, widths other than d_model = 256 / d_ff <= 768, SCA_CHAIN_NEXT=0)."""
-    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "qkv" or drop_p(ffns) > 0:
+    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "qkv" or drop_p(ffns) > 0 or library.compiling():
         return None
     specs = [[(f.fc1.weight, f.fc1.bias, 1.0, True)] for f in ffns]
     return ops.NextProjections(specs) if ops.NextProjections.eligible(specs) else None
@@ -93,7 +93,7 @@ def coordinate_mapping_grouped(maps, keypoints, joint_idx):
     """G streams sliced out of ONE (B, T, K_all, 2) keypoint tensor (model/__init__.py:133-142)
     and mapped (layers.py:118-123) in one launch.  joint_idx: list of int32 device tensors."""
     G = len(maps)
-    out = ops.CoordinateMappingOp.apply(G, keypoints, *joint_idx, *[m.mapping_x.weight for m in maps],
+    out = library.coordinate_mapping_apply(G, keypoints, *joint_idx, *[m.mapping_x.weight for m in maps],
                                         *[m.mapping_x.bias for m in maps], *[m.mapping_y.weight for m in maps],
                                         *[m.mapping_y.bias for m in maps])
     return list(out[:G]), list(out[G:])

@@ -286,7 +286,7 @@ class LnSaved:
 
 def ln_saved_of(ts):
     """Consumer forward: the LnSaved of each input (all G or None)."""
-    if not _FUSE_LNB:
+    if not _FUSE_LNB or _LIBRARY_MODE:
         return None
     out = [getattr(t, "_sca_ln", None) for t in ts]
     return out if all(o is not None for o in out) else None
@@ -307,6 +307,8 @@ def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None, aux=None):
     ok = wo is not None and _CHAIN_DO and all(
         w.dim() == 2 and w.shape[0] == 256 and w.shape[1] % 256 == 0 and w.shape[1] <= 768 and w.is_contiguous()
         for w in wo)
+    if _LIBRARY_MODE:
+        return None
     objs = [LnSaved(vs[g], means[g], rstds[g], gam[g], wo[g] if ok else None,
                     aux[g] if (ok and aux is not None) else None)
             for g in range(len(ys))]
@@ -614,6 +616,23 @@ def set_grad_sink(sink):
     _GRAD_SINK = sink
 
 
+# library mode (scattennet_amd.library's torch.library operators): the grouped Functions'
+# bodies run for one stream, as pure functions of their operands — no cross-op hand-offs,
+# no weight-gradient side stream, no gradient sink
+_LIBRARY_MODE = False
+
+
+class library_mode:
+    def __enter__(self):
+        global _LIBRARY_MODE, _GRAD_SINK
+        self.prev = (_LIBRARY_MODE, _GRAD_SINK)
+        _LIBRARY_MODE, _GRAD_SINK = True, None
+
+    def __exit__(self, *exc):
+        global _LIBRARY_MODE, _GRAD_SINK
+        _LIBRARY_MODE, _GRAD_SINK = self.prev
+
+
 def param_grad_empty(p):
     if _GRAD_SINK is not None:
         t = _GRAD_SINK.grad_buffer(p)
@@ -828,7 +847,7 @@ def weight_grads(items, M=None, extra=None):
     # a parameter that already holds a .grad gets the new gradient added by autograd as soon
     # as this returns (ordered on the current stream only): compute on the current stream
     params = [it[3] for it in items] + list(extra[2] if extra is not None else ())
-    if not _WGRAD_SIDE or any(p.grad is not None for p in params):
+    if not _WGRAD_SIDE or _LIBRARY_MODE or any(p.grad is not None for p in params):
         return run()
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
@@ -1396,7 +1415,8 @@ class LayerNormAdd(Function):
         # the embedding LayerNorm (position table, no tail, no dropout): its backward can ride
         # in the consuming attention block's input-gradient GEMM (sca_gemm_lnb, tab mode)
         ctx.lnsaved = None
-        if pos_table and not has_post and not act and drop_p == 0 and ln_width_ok(N) and _FUSE_LNB and _EMB_LNB:
+        if (pos_table and not has_post and not act and drop_p == 0 and ln_width_ok(N) and _FUSE_LNB and _EMB_LNB and
+                not _LIBRARY_MODE):
             ctx.lnsaved = [LnSaved(x[g], means[g], rstds[g], gam[g], tab=tab[g], T=T) for g in range(G)]
             for y, o in zip(ys, ctx.lnsaved):
                 y._sca_ln = o

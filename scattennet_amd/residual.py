@@ -5,7 +5,7 @@ frame-axis max-pool kernel."""
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import library, ops
 from .layers import layernorm_grouped
 
 
@@ -34,7 +34,7 @@ class ResidualBlock(nn.Module):
 
 def _linear(layers, xs):
     G = len(xs)
-    return list(ops.LinearResidual.apply(G, False, *xs, *[l.weight for l in layers], *[l.bias for l in layers]))
+    return list(library.linear_apply(G, False, *xs, *[l.weight for l in layers], *[l.bias for l in layers]))
 
 
 def residual_block_grouped(blocks, xs):
@@ -46,7 +46,7 @@ def residual_block_grouped(blocks, xs):
     h = _linear([b.linear2 for b in blocks], h)
     h = layernorm_grouped([b.norm2 for b in blocks], h, post=r, relu=True)
     if b0.downsample:
-        h = list(ops.MaxPoolT.apply(len(h), *h))
+        h = list(library.maxpool_t_apply(len(h), *h))
     return h
 
 
