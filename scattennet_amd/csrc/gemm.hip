@@ -705,6 +705,281 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
   SCA_STAMP(3);
 }
 
+// ------------------------------------------------------------------------------ TN, k-split waves
+// Weight-gradient GEMM (TN: dW[M x N] = A^T B over K rows; A = dY [K][M], B = X [K][N], both
+// k-major, the LDS-DMA ring of gemm_glds_kernel) with 16x16x4 MFMAs in an outer-product form:
+// a lane's float4 of A (4 consecutive m at one k) and of B (4 consecutive n) feed 16 MFMAs,
+// MFMA (i, j) taking A's component i and B's component j, i.e. the tile rows m = 4a + i and
+// columns n = 4b + j (a, b = the lane's index within 16).  Every wave accumulates the FULL
+// 64x64 tile over its quarter of each K slice — one ds_read_b128 per operand per 16 MFMAs,
+// where the 32x32x2 form reads 4 ds_read_b32 per fragment — and the 4 waves' partial tiles
+// are summed in fixed order through LDS.  A lane ends with tile rows 16g .. 16g+15 x columns
+// 4c .. 4c+3 (g = lane >> 4, c = lane & 15).  Epilogue, split-K slabs and in-launch combine
+// as gemm_glds_kernel (same 32x32 quadrant row layout after the reduction).
+constexpr int TNK_PLD = 68;  // partial-tile row stride (floats): 16-B shift per row
+constexpr int TNK_RED = 4 * 64 * TNK_PLD * 4 + 4 * 64 * 4;  // 4 partial tiles + 4 bias partial rows
+
+// SUB: K slices per ring stage (one wait + barrier per SUB x 32 k rows); PF (SUB = 1): the
+// fragments of slice t+1 are read from LDS during slice t's MFMAs (register double buffer)
+template <int S, int SUB, bool PF = false, int NODMA = 0>
+__global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
+  constexpr int SLICE = 2 * GL_OP_BYTES;
+  constexpr int STAGE = SUB * SLICE;
+  constexpr int SMEM = S * STAGE > TNK_RED ? S * STAGE : TNK_RED;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
+
+  const int splitk = args.splitk;
+  const int pid = bz / splitk;
+  const int ks = bz % splitk;
+  const sca_gemm_problem& P = args.p[pid];
+  const int m0 = by * GL_BM, n0 = bx * GL_BN;
+  if (m0 >= P.M || n0 >= P.N) return;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+
+  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
+    seg_kbeg[s] = seg_n[s] = 0;
+    if (s < P.nseg) {
+      int kbeg = 0, kend = P.seg[s].K;
+      if (splitk > 1) {
+        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + GL_BK - 1) / GL_BK * GL_BK;
+        kbeg = ks * chunk;
+        kend = min(P.seg[s].K, kbeg + chunk);
+      }
+      seg_kbeg[s] = kbeg;
+      seg_n[s] = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
+      total += seg_n[s];
+    }
+  }
+  int iseg = -1, tseg0 = 0, tend = 0;
+  const float* pa[2] = {nullptr, nullptr};
+  const float* pb[2] = {nullptr, nullptr};
+  long stepA = 0, stepB = 0;
+  auto dma = [&](int t, int stage) {
+    while (t >= tend) {
+      ++iseg;
+      tseg0 = tend;
+      tend += seg_n[iseg];
+      const sca_gemm_seg& G = P.seg[iseg];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        pa[q] = gl_src<false>(G.A, G.lda, m0, P.M, seg_kbeg[iseg], q, wave, lane);
+        pb[q] = gl_src<false>(G.B, G.ldb, n0, P.N, seg_kbeg[iseg], q, wave, lane);
+      }
+      stepA = (long)GL_BK * G.lda;
+      stepB = (long)GL_BK * G.ldb;
+    }
+    const long kk = t - tseg0;
+    char* base = smem + stage * STAGE + (t % SUB) * SLICE;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      gl_dma(pa[q] + kk * stepA, base + gl_dst<false>(q, wave));
+      gl_dma(pb[q] + kk * stepB, base + GL_OP_BYTES + gl_dst<false>(q, wave));
+    }
+  };
+  const int nst = (total + SUB - 1) / SUB;  // ring stages to walk
+  auto dma_stage = [&](int u, int stage) {
+#pragma unroll
+    for (int q = 0; q < SUB; ++q)
+      if (u * SUB + q < total) dma(u * SUB + q, stage);
+  };
+
+  const bool do_bias = P.bias_grad != nullptr && bx == 0;
+  f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto frags = [&](const char* stage, f32x4 (&a)[2], f32x4 (&b)[2]) {
+    const float* As = reinterpret_cast<const float*>(stage);
+    const float* Bs = As + GL_BM * GL_BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 4 * (2 * wave + h) + g;  // image row: this wave's k quarter of the slice
+      a[h] = ld4(As + k * GL_BM + 4 * c);
+      b[h] = ld4(Bs + k * GL_BN + 4 * c);
+    }
+  };
+  auto mma = [&](const f32x4 (&a)[2], const f32x4 (&b)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (do_bias) bs4 += a[h];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[h][i], b[h][j], acc[i][j]);
+    }
+  };
+  if constexpr (PF) {
+    static_assert(SUB == 1 && S >= 2, "PF: one slice per stage");
+    // iteration t: slice t+1 landed (every wave also holds slice t's fragments: lgkmcnt(0)),
+    // barrier, DMA slice t+S into slice t's stage, read slice t+1's fragments, MFMAs of t
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (i < total) dma(i, i);
+    f32x4 ca[2], cb[2], na[2], nb[2];
+    if (total > 0) {
+      if (total >= S) gl_wait_vm<4 * (S - 1)>();  // slice 0 landed (slices 1 .. S-1 may fly)
+      else gl_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      frags(smem, ca, cb);
+    }
+    for (int t = 0; t < total; ++t) {
+      if (t + 1 < total) {
+        // slice t+1 landed: the slices issued after it (up to t+S-1) may still fly
+        const int younger = min(total - 1, t + S - 1) - (t + 1);
+        if (younger >= S - 2) gl_wait_vm<4 * (S - 2)>();
+        else gl_wait_vm<0>();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): slice t's fragments are in registers
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (!NODMA && t + S < total) dma(t + S, t % S);
+        frags(smem + ((t + 1) % S) * STAGE, na, nb);
+      }
+      mma(ca, cb);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ca[h] = na[h];
+        cb[h] = nb[h];
+      }
+    }
+  } else {
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nst) dma_stage(i, i);
+  // stage u landed: the younger in-flight stages hold 4 SUB pieces each, except a partial
+  // last stage (then wait for everything)
+  const bool whole = total % SUB == 0;
+  for (int u = 0; u < nst; ++u) {
+    if (u + S - 2 < nst && (whole || u + S - 2 < nst - 1)) gl_wait_vm<4 * SUB * (S - 2)>();
+    else gl_wait_vm<0>();
+    if (NODMA < 2) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if ((NODMA == 0 || NODMA == 3) && u + S - 1 < nst) dma_stage(u + S - 1, (u + S - 1) % S);  // NODMA: probes
+#pragma unroll
+    for (int q = 0; q < SUB; ++q) {
+      if (u * SUB + q >= total) break;
+      const float* As = reinterpret_cast<const float*>(smem + (u % S) * STAGE + q * SLICE);
+      const float* Bs = As + GL_BM * GL_BK;
+      f32x4 a[2], b[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = 4 * (2 * wave + h) + g;  // image row: this wave's k quarter of the slice
+        a[h] = ld4(As + k * GL_BM + 4 * c);
+        b[h] = ld4(Bs + k * GL_BN + 4 * c);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (do_bias) bs4 += a[h];
+        if (NODMA == 3) {  // memory-pipeline probe: consume the fragments without MFMAs
+          acc[0][0] += a[h] + b[h];
+          continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[h][i], b[h][j], acc[i][j]);
+      }
+    }
+  }
+  }
+
+  // the 4 waves' partial tiles (and bias rows) through LDS, summed in fixed order per quadrant
+  __syncthreads();  // the ring is free
+  float* red = reinterpret_cast<float*>(smem);
+  float* mine = red + wave * 64 * TNK_PLD;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      st4(mine + (16 * g + 4 * r + i) * TNK_PLD + 4 * c, f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]});
+  float* bred = red + 4 * 64 * TNK_PLD;
+  if (do_bias) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bs4[q] += __shfl_xor(bs4[q], 16, 64);
+      bs4[q] += __shfl_xor(bs4[q], 32, 64);
+    }
+    if (g == 0) st4(bred + wave * 64 + 4 * c, bs4);
+  }
+  __syncthreads();
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const float alpha = P.seg[0].alpha;
+  f32x4 rows[4];
+#pragma unroll
+  for (int i4 = 0; i4 < 4; ++i4) {
+    const int e = (wm + (lane >> 3) + 8 * i4) * TNK_PLD + wn + 4 * (lane & 7);
+    rows[i4] = ((ld4(red + e) + ld4(red + 64 * TNK_PLD + e)) + ld4(red + 2 * 64 * TNK_PLD + e)) +
+               ld4(red + 3 * 64 * TNK_PLD + e);
+    if (alpha != 1.f) rows[i4] *= alpha;
+  }
+  const bool fused_k = splitk > 1 && args.counters != nullptr;
+  if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
+    const int br = threadIdx.x;
+    const float bsum = ((bred[br] + bred[64 + br]) + bred[128 + br]) + bred[192 + br];
+    float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m0 + br;
+    if (fused_k)
+      __hip_atomic_store(bp, bsum * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
+    else if (splitk > 1)
+      *bp = bsum * alpha;
+    else
+      P.bias_grad[m0 + br] = bsum * alpha * P.bias_grad_scale;
+  }
+  if (fused_k) {
+    const long MN = (long)P.M * P.N;
+    float* slabs = args.ws + args.slab_off[pid];
+    slab_rows_sc1(slabs, (long)splitk * MN, rows, P.M, P.N, m0 + wm, n0 + wn, lane, (long)ks * MN);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(smem);  // the partial tiles are consumed
+    unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
+    const int n = n0 + wn + 4 * (lane & 7);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = min(m0 + wm + (lane >> 3) + 8 * i, P.M - 1);
+      const long e = (long)m * P.N + min(n, P.N - 4);
+      f32x4 tt = ld4_sc1(rs, e);
+      for (int s2 = 1; s2 < splitk; ++s2) tt += ld4_sc1(rs, s2 * MN + e);
+      rows[i] = tt;
+    }
+    if (do_bias && threadIdx.x < GL_BM && m0 + (int)threadIdx.x < P.M) {
+      float* bp = args.ws + args.bias_off[pid] + m0 + threadIdx.x;
+      float tt = 0.f;
+      for (int s2 = 0; s2 < splitk; ++s2)
+        tt += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P.bias_grad[m0 + threadIdx.x] = tt * P.bias_grad_scale;
+    }
+    epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
+    return;
+  }
+  if (splitk > 1) {
+    slab_rows(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N, rows, P.M, P.N, m0 + wm, n0 + wn, lane);
+    return;
+  }
+  epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
+}
+
 // ------------------------------------------------------------------------------ LDS-DMA, 8 waves
 // gemm_glds_kernel's 64x64 tile with TWO 4-wave groups that split the K-slices of the tile
 // between them (group g computes slices g, g+2, ...; the ring stage holds one slice per
@@ -2277,7 +2552,15 @@ using TN2 = TnCfg<64, 64, 2, 2, 4, 0, true>;    // 4 waves, fragments one slice 
 using TN3 = TnCfg<64, 64, 2, 2, 4, 4, true>;    // + 4 loader waves, fragments one slice ahead
 using TN4 = TnCfg<128, 64, 2, 2, 4, 4, true>;   // 4 compute waves 64x32 + 4 loaders, prefetch
 using TN5 = TnCfg<64, 64, 2, 2, 3, 4, true>;    // 3 stages + 4 loaders, prefetch
-constexpr int kTnFirst = 30, kTnLast = 35;
+// 36 .. 39: gemm_tnk_kernel, ring stages 3 / 4, fragments read in-slice (36, 37) or one slice ahead (38, 39)
+constexpr int kTnFirst = 30, kTnLast = 43;
+
+template <int S, int SUB, bool PF = false, int NODMA = 0>
+int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
+  hipLaunchKernelGGL((gemm_tnk_kernel<S, SUB, PF, NODMA>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
 
 template <class C>
 int launch_tn(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
@@ -2305,7 +2588,15 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
         case 32: return launch_tn<TN2>(a, nprob, maxM, maxN, st);
         case 33: return launch_tn<TN3>(a, nprob, maxM, maxN, st);
         case 34: return launch_tn<TN4>(a, nprob, maxM, maxN, st);
-        default: return launch_tn<TN5>(a, nprob, maxM, maxN, st);
+        case 35: return launch_tn<TN5>(a, nprob, maxM, maxN, st);
+        case 36: return launch_tnk<3, 1>(a, nprob, maxM, maxN, st);
+        case 37: return launch_tnk<4, 1>(a, nprob, maxM, maxN, st);
+        case 38: return launch_tnk<3, 1, true>(a, nprob, maxM, maxN, st);
+        case 39: return launch_tnk<4, 1, true>(a, nprob, maxM, maxN, st);
+        case 40: return launch_tnk<3, 1, false, 1>(a, nprob, maxM, maxN, st);  // timing probes
+        case 41: return launch_tnk<3, 1, true, 1>(a, nprob, maxM, maxN, st);
+        case 42: return launch_tnk<3, 1, false, 2>(a, nprob, maxM, maxN, st);
+        default: return launch_tnk<3, 1, false, 3>(a, nprob, maxM, maxN, st);
       }
     }
   }

@@ -198,8 +198,22 @@ def _splitk_counters(n, device=None):
     return ring[pos:pos + n]
 
 
-def gemm(layout, probs, splitk=1, ws=None):
+_TILE_NAMES = {36: "gemm_tnk_kernel<3, 1, false, 0>", 37: "gemm_tnk_kernel<4, 1, false, 0>"}
+
+
+def gemm(layout, probs, splitk=1, ws=None, tile=0):
+    """tile: a kernel variant for this call only (sca_gemm_tile_override ids; 0 = the heuristic)."""
     lib = L.lib()
+    if tile:
+        L.check(lib.sca_gemm_tile_override(layout, tile), "sca_gemm_tile_override")
+        try:
+            return _gemm(lib, layout, probs, splitk, ws, _TILE_NAMES.get(tile, f"gemm tile {tile}"))
+        finally:
+            lib.sca_gemm_tile_override(layout, _TN_TILE if layout == L.GEMM_TN else 0)
+    return _gemm(lib, layout, probs, splitk, ws, _GEMM_NAMES[layout])
+
+
+def _gemm(lib, layout, probs, splitk, ws, kname):
     st = L.stream_handle()
     for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
@@ -209,11 +223,11 @@ def gemm(layout, probs, splitk=1, ws=None):
             cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
                                                                 max(p.N for p in chunk)),
                                    ws.device.index if ws is not None else None)
-            with _timed(_GEMM_NAMES[layout], flops):
+            with _timed(kname, flops):
                 L.check(lib.sca_gemm_splitk_fused(layout, len(chunk), arr, splitk, ptr(ws), ptr(cnt), st),
                         "sca_gemm_splitk_fused")
             continue
-        with _timed(_GEMM_NAMES[layout], flops):
+        with _timed(kname, flops):
             L.check(lib.sca_gemm_partial(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm")
         if splitk > 1:  # the fixed-order slab reduction: its own launch (timed apart)
             with _timed("splitk_reduce4_kernel", 0.0):
@@ -594,6 +608,9 @@ def _splitk_for(M_red, n_out_tiles):
 
 
 _SPLITK_MAX = int(__import__("os").environ.get("SCA_SPLITK_MAX", "8"))
+# many-problem weight-gradient launches on gemm_tnk_kernel (+0.2-0.6 % in step, three
+# alternations, tools/r03_t16.sh); SCA_TNK_MANY=0: every TN launch on the LDS-DMA kernel
+_TNK_MANY = __import__("os").environ.get("SCA_TNK_MANY", "1") != "0"
 _SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
 _WGRAD_MIX = __import__("os").environ.get("SCA_WGRAD_MIX", "0") != "0"
 _SPLITK_ROUNDS = __import__("os").environ.get("SCA_SPLITK_ROUNDS", "1") != "0"
@@ -912,6 +929,12 @@ def _weight_grads(items, deferred=False):
             tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
             _tn_setup()
             sk = _TN_SPLITK if _TN_SPLITK > 0 else _splitk_for(items[sub[0]][0].shape[0], tiles)
+            tile = 0
+            if _TNK_MANY and not _TN_TILE and len(sub) >= 8 and tiles >= 256:
+                # many-problem launches (an attention block's q/k/v/o of every stream): the
+                # k-split outer-product kernel at split-K 2 (tools/tn_bench.py: 16 x (256 x 256,
+                # K = 2048) 0.59-0.61 of peak vs 0.57 for the 64x64 LDS-DMA kernel at split 3)
+                tile, sk = 36, 2
             probs, wsz = [], 0
             for i in sub:
                 dY, X, alpha, W, _, bscale = items[i]
@@ -921,11 +944,11 @@ def _weight_grads(items, deferred=False):
                                    bias_grad=out[i][1], bias_grad_scale=bscale / alpha))
                 wsz += sk * (n_out * n_in + n_out)
             ws = torch.empty(wsz, device=items[0][0].device, dtype=torch.float32) if sk > 1 else None
-            launches.append((probs, sk, ws))
+            launches.append((probs, sk, ws, tile))
     if deferred:
-        return out, lambda: [gemm(L.GEMM_TN, p, splitk=k, ws=w) for p, k, w in launches]
-    for p, k, w in launches:
-        gemm(L.GEMM_TN, p, splitk=k, ws=w)
+        return out, lambda: [gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl) for p, k, w, tl in launches]
+    for p, k, w, tl in launches:
+        gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl)
     return out
 
 

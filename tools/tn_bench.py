@@ -17,8 +17,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-NAMES = {21: "glds64", 30: "T64s4", 31: "T64+4L", 32: "T64pf", 33: "T64pf+4L", 34: "T128x64pf+4L", 35: "T64s3pf+4L"}
-TILE_BM = {21: (64, 64), 30: (64, 64), 31: (64, 64), 32: (64, 64), 33: (64, 64), 34: (128, 64), 35: (64, 64)}
+NAMES = {21: "glds64", 30: "T64s4", 31: "T64+4L", 32: "T64pf", 33: "T64pf+4L", 34: "T128x64pf+4L", 35: "T64s3pf+4L",
+         36: "TNKs3", 37: "TNKs4", 38: "TNKs3pf", 39: "TNKs4pf", 40: "probe-noDMA", 41: "probe-pf-noDMA", 42: "probe-noDMA-nobar", 43: "probe-DMA-noMFMA"}
+TILE_BM = {21: (64, 64), 30: (64, 64), 31: (64, 64), 32: (64, 64), 33: (64, 64), 34: (128, 64), 35: (64, 64),
+           36: (64, 64), 37: (64, 64), 38: (64, 64), 39: (64, 64), 40: (64, 64), 41: (64, 64), 42: (64, 64), 43: (64, 64)}
 
 
 def make_case(name, shapes, Mr=2048):
@@ -77,7 +79,8 @@ def main():
                 for (_, _, dW, db), (rw, rb) in zip(c["items"], c["ref"]):
                     ew = float((dW.double().cpu() - rw).abs().max() / rw.abs().max())
                     eb = float((db.double().cpu() - rb).abs().max() / rb.abs().max())
-                    assert ew < 1e-5 and eb < 1e-5, (c["name"], t, sk, ew, eb)
+                    if t not in (40, 41, 42, 43):  # 40, 41: the no-DMA timing probes computes garbage by design
+                        assert ew < 1e-5 and eb < 1e-5, (c["name"], t, sk, ew, eb)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for _ in range(args.iters):
