@@ -294,7 +294,7 @@ int sca_attn_bwd_fused(int enable);
  * drop_p > 0 (act must be identity): y = dropout(y) with the sca_dropout mask of
  * drop_seed — the embedding dropout after first_*_norm (keypoint_module.py:164-165); the
  * backward applies the same mask to dy (sca_dropout) before sca_layernorm_bwd.
- * Saves mean/rstd per row.                                                              */
+ * Saves mean/rstd per row.  Any N (widths over 1024 take a row-looping kernel).         */
 #define SCA_ACT_NONE 0
 #define SCA_ACT_RELU 1
 typedef struct {
@@ -348,7 +348,7 @@ typedef struct {
 int sca_maxpool_t_fwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream);
 int sca_maxpool_t_bwd(int nprob, const sca_pool_problem* probs, int B, int T, int C, void* stream);
 
-/* Row softmax over the last dim (N <= 1024) and its backward (CoordinatesFusion's
+/* Row softmax over the last dim (any N) and its backward (CoordinatesFusion's
  * unscaled, unmasked attention weights, model/fusion.py:52-53):
  *   fwd: y = softmax(x)            bwd: dx = y * (dy - sum_j dy_j y_j)                  */
 typedef struct {

@@ -341,6 +341,133 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const SoftmaxArgs a) {
   store_row<NV>(P.out + (long)row * N, g, lane, N);
 }
 
+// Wide rows (N > 1024, any N): one wave per row looping over the row in 64-column strides —
+// the sum, the squared deviations and the output each re-read the row (L2-resident between
+// the passes); same two-pass statistics as the register kernels above.
+__global__ __launch_bounds__(256) void ln_fwd_wide_kernel(const LnFwdArgs a) {
+  const sca_ln_fwd_problem& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int N = a.N;
+  const float* x = P.x + (long)row * N;
+  const float* r = P.r ? P.r + rrow(row, a.r_mod, a.r_off) * N : nullptr;
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s += r ? x[c] + r[c] : x[c];
+  const float mean = wave_sum(s) / N;
+  float q = 0.f;
+  for (int c = lane; c < N; c += 64) {
+    const float d = (r ? x[c] + r[c] : x[c]) - mean;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / N + a.eps);
+  DropMask dm;
+  if (P.drop_p > 0.f) dm.init(P.drop_seed, P.drop_p, a.drop_off);
+  const float* post = P.post ? P.post + (long)row * N : nullptr;
+  float* y = P.y + (long)row * N;
+  for (int c = lane; c < N; c += 64) {
+    float o = ((r ? x[c] + r[c] : x[c]) - mean) * rstd * P.gamma[c] + P.beta[c];
+    if (post) o += post[c];
+    if (P.act == SCA_ACT_RELU) o = fmaxf(o, 0.f);
+    if (P.drop_p > 0.f) o = dm.apply((uint32_t)row * (uint32_t)N + (uint32_t)c, o);
+    y[c] = o;
+  }
+  if (lane == 0) {
+    P.mean[row] = mean;
+    P.rstd[row] = rstd;
+  }
+}
+
+// Wide-row backward: a workgroup takes LN_BWD_ROWS rows; phase 1 (one wave per row) the two
+// row sums of dy*gamma and dy*gamma*x-hat, phase 2 (thread per column, rows in order) dx and
+// the workgroup's dgamma / dbeta partial row.
+__global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const LnBwdArgs a) {
+  const sca_ln_bwd_problem& P = a.p[blockIdx.y];
+  __shared__ float st[2][LN_BWD_ROWS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int N = a.N;
+  const int rbeg = blockIdx.x * LN_BWD_ROWS;
+  auto gated = [&](int row, int c) {  // dy with the ReLU gate (threshold_backward: out > 0)
+    const float d = P.dy[(long)row * N + c];
+    return P.act && !(P.y[(long)row * N + c] > 0.f) ? 0.f : d;
+  };
+  auto xin = [&](int row, int c) {
+    const float v = P.x[(long)row * N + c];
+    return P.r ? v + P.r[rrow(row, a.r_mod, a.r_off) * N + c] : v;
+  };
+  for (int rr = w; rr < LN_BWD_ROWS; rr += 4) {
+    const int row = rbeg + rr;
+    if (row >= a.rows) break;
+    const float mean = P.mean[row], rstd = P.rstd[row];
+    float sg = 0.f, sgx = 0.f;
+    for (int c = lane; c < N; c += 64) {
+      const float d = gated(row, c);
+      if (P.dpost) P.dpost[(long)row * N + c] = d;
+      const float g = d * P.gamma[c];
+      sg += g;
+      sgx += g * (xin(row, c) - mean) * rstd;
+    }
+    sg = wave_sum(sg);
+    sgx = wave_sum(sgx);
+    if (lane == 0) {
+      st[0][rr] = sg / N;
+      st[1][rr] = sgx / N;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += 256) {
+    const float gam = P.gamma[c];
+    float pg = 0.f, pb = 0.f;
+    for (int rr = 0; rr < LN_BWD_ROWS; ++rr) {
+      const int row = rbeg + rr;
+      if (row >= a.rows) break;
+      const float d = gated(row, c);
+      const float xh = (xin(row, c) - P.mean[row]) * P.rstd[row];
+      float dx = P.rstd[row] * (d * gam - st[0][rr] - xh * st[1][rr]);
+      float* dxp = P.dx + (long)row * N + c;
+      if (a.accumulate) dx += *dxp;
+      *dxp = dx;
+      pg += d * xh;
+      pb += d;
+    }
+    P.partial[(long)blockIdx.x * N + c] = pg;
+    P.partial[((long)a.nblk + blockIdx.x) * N + c] = pb;
+  }
+}
+
+// Wide-row softmax (N > 1024): one wave per row, max / sum / output passes over the row.
+__global__ __launch_bounds__(256) void softmax_fwd_wide_kernel(const SoftmaxArgs a) {
+  const sca_softmax_problem& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int N = a.N;
+  const float* x = P.x + (long)row * N;
+  float m = -INFINITY;
+  for (int c = lane; c < N; c += 64) m = fmaxf(m, x[c]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s += __expf(x[c] - m);
+  const float inv = 1.0f / wave_sum(s);
+  float* o = P.out + (long)row * N;
+  for (int c = lane; c < N; c += 64) o[c] = __expf(x[c] - m) * inv;
+}
+
+__global__ __launch_bounds__(256) void softmax_bwd_wide_kernel(const SoftmaxArgs a) {
+  const sca_softmax_problem& P = a.p[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int N = a.N;
+  const float* y = P.y + (long)row * N;
+  const float* g = P.dy + (long)row * N;
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s += y[c] * g[c];
+  s = wave_sum(s);
+  float* o = P.out + (long)row * N;
+  for (int c = lane; c < N; c += 64) o[c] = y[c] * (g[c] - s);
+}
+
 // ------------------------------------------------------------------------------ GELU backward
 struct GeluArgs {
   sca_gelu_bwd_problem p[SCA_GELU_MAX_PROBLEMS];
@@ -695,8 +822,8 @@ extern "C" void sca_set_error(const char* msg);
 
 extern "C" int sca_layernorm_fwd(int nprob, const sca_ln_fwd_problem* probs, int rows, int N, int r_mod,
                                  int r_off, float eps, void* stream) {
-  if (nprob < 1 || nprob > SCA_LN_MAX_PROBLEMS || N < 1 || N > 64 * LN_MAXV || rows < 0 || r_mod < 1) {
-    sca_set_error("sca_layernorm_fwd: bad arguments (N must be <= 1024)");
+  if (nprob < 1 || nprob > SCA_LN_MAX_PROBLEMS || N < 1 || rows < 0 || r_mod < 1) {
+    sca_set_error("sca_layernorm_fwd: bad arguments");
     return SCA_ERR_ARG;
   }
   if (rows == 0) return SCA_OK;
@@ -712,7 +839,8 @@ extern "C" int sca_layernorm_fwd(int nprob, const sca_ln_fwd_problem* probs, int
   a.drop_off = sca_drop_offset_ptr();
   dim3 grid((rows + 3) / 4, nprob);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  switch (N % 256 == 0 ? N / 256 : 0) {
+  switch (N > 64 * LN_MAXV ? -1 : N % 256 == 0 ? N / 256 : 0) {
+    case -1: hipLaunchKernelGGL(ln_fwd_wide_kernel, grid, dim3(256), 0, st, a); break;
     case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, a); break;
     case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, a); break;
     case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, dim3(256), 0, st, a); break;
@@ -757,7 +885,7 @@ extern "C" int sca_maxpool_t_bwd(int nprob, const sca_pool_problem* probs, int B
 
 template <bool BWD>
 int launch_softmax(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream, const char* what) {
-  if (nprob < 1 || nprob > SCA_SOFTMAX_MAX_PROBLEMS || rows < 0 || N < 1 || N > 64 * LN_MAXV) {
+  if (nprob < 1 || nprob > SCA_SOFTMAX_MAX_PROBLEMS || rows < 0 || N < 1) {
     sca_set_error(what);
     return SCA_ERR_ARG;
   }
@@ -772,7 +900,10 @@ int launch_softmax(int nprob, const sca_softmax_problem* probs, int rows, int N,
 #define SCA_SM(NVV)                                                                   \
   if (BWD) hipLaunchKernelGGL(softmax_bwd_kernel<NVV>, grid, dim3(256), 0, st, a);   \
   else hipLaunchKernelGGL(softmax_fwd_kernel<NVV>, grid, dim3(256), 0, st, a);
-  switch (nv) {
+  if (N > 64 * LN_MAXV) {
+    if (BWD) hipLaunchKernelGGL(softmax_bwd_wide_kernel, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(softmax_fwd_wide_kernel, grid, dim3(256), 0, st, a);
+  } else switch (nv) {
     case 1: SCA_SM(1) break;
     case 2: SCA_SM(2) break;
     case 3: SCA_SM(3) break;
@@ -785,11 +916,11 @@ int launch_softmax(int nprob, const sca_softmax_problem* probs, int rows, int N,
 }
 
 extern "C" int sca_softmax_rows_fwd(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream) {
-  return launch_softmax<false>(nprob, probs, rows, N, stream, "sca_softmax_rows_fwd: bad arguments (N <= 1024)");
+  return launch_softmax<false>(nprob, probs, rows, N, stream, "sca_softmax_rows_fwd: bad arguments");
 }
 
 extern "C" int sca_softmax_rows_bwd(int nprob, const sca_softmax_problem* probs, int rows, int N, void* stream) {
-  return launch_softmax<true>(nprob, probs, rows, N, stream, "sca_softmax_rows_bwd: bad arguments (N <= 1024)");
+  return launch_softmax<true>(nprob, probs, rows, N, stream, "sca_softmax_rows_bwd: bad arguments");
 }
 
 extern "C" int sca_gelu_bwd(int nprob, const sca_gelu_bwd_problem* probs, long n, void* stream) {
@@ -819,7 +950,7 @@ extern "C" int sca_layernorm_bwd_blocks(int rows) { return (rows + LN_BWD_ROWS -
 
 extern "C" int sca_layernorm_bwd(int nprob, const sca_ln_bwd_problem* probs, int rows, int N, int r_mod,
                                  int r_off, int accumulate, void* stream) {
-  if (nprob < 1 || nprob > SCA_LN_MAX_PROBLEMS || N < 1 || N > 64 * LN_MAXV || rows < 1 || r_mod < 1) {
+  if (nprob < 1 || nprob > SCA_LN_MAX_PROBLEMS || N < 1 || rows < 1 || r_mod < 1) {
     sca_set_error("sca_layernorm_bwd: bad arguments");
     return SCA_ERR_ARG;
   }
@@ -828,7 +959,8 @@ extern "C" int sca_layernorm_bwd(int nprob, const sca_ln_bwd_problem* probs, int
   a.rows = rows; a.N = N; a.r_mod = r_mod; a.r_off = r_off; a.accumulate = accumulate;
   a.nblk = sca_layernorm_bwd_blocks(rows);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  switch (N % 256 == 0 ? N / 256 : 0) {
+  switch (N > 64 * LN_MAXV ? -1 : N % 256 == 0 ? N / 256 : 0) {
+    case -1: hipLaunchKernelGGL(ln_bwd_wide_kernel, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
     case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
     case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;
     case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(a.nblk, nprob), dim3(256), 0, st, a); break;

@@ -995,11 +995,41 @@ def _mask_heads(add_mask):
     return add_mask.shape[1] if add_mask is not None and add_mask.dim() == 4 else 1
 
 
+_KERNEL_HD = (16, 32, 64)  # head sizes the attention kernels are built for
+
+
+def _padded_hd(hd):
+    """Kernel head size for a module head size: hd itself, or the next kernel size when the
+    heads are zero-padded (exact: zero q / k columns add nothing to a score, zero v columns
+    give zero output columns and the padded gradient columns are dropped)."""
+    for k in _KERNEL_HD:
+        if hd <= k:
+            return k
+    raise ValueError(f"head_dim {hd} > {_KERNEL_HD[-1]} is not supported by the attention kernels")
+
+
+def _pad_heads(ts, H, hd, hdp):
+    """(B, T, H*hd) -> (B, T, H*hdp), each head's columns followed by hdp - hd zeros."""
+    return [torch.nn.functional.pad(t.reshape(t.shape[0], t.shape[1], H, hd), (0, hdp - hd))
+            .reshape(t.shape[0], t.shape[1], H * hdp) for t in ts]
+
+
+def _unpad_heads(ts, H, hd, hdp):
+    return [t.reshape(t.shape[0], t.shape[1], H, hdp)[..., :hd].reshape(t.shape[0], t.shape[1], H * hd)
+            for t in ts]
+
+
 def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
-    """drop: None or (p, seeds) — attention-probability dropout, one seed per problem."""
+    """drop: None or (p, seeds) — attention-probability dropout, one seed per problem.
+    Head sizes other than 16 / 32 / 64 run zero-padded to the next kernel size."""
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
+    hdp = _padded_hd(hd)
+    if hdp != hd:
+        qp, kp, vp = (_pad_heads(ts, H, hd, hdp) for ts in (q, k, v))
+        o, sm, sl = _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, qp, kp, vp, drop)
+        return _unpad_heads(o, H, hd, hdp), sm, sl
     o = [torch.empty_like(t) for t in q]
     sm = [q[0].new_empty(B * H * Tq) for _ in range(G)]
     sl = [q[0].new_empty(B * H * Tq) for _ in range(G)]
@@ -1021,6 +1051,12 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
+    hdp = _padded_hd(hd)
+    if hdp != hd:
+        qp, kp, vp, op, dop = (_pad_heads(ts, H, hd, hdp) for ts in (q, k, v, o, dout))
+        grads = _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, qp, kp, vp, op, sm, sl, dop, dq_scale,
+                          dv_scale, drop)
+        return tuple(_unpad_heads(g, H, hd, hdp) for g in grads)
     dq = [torch.empty_like(t) for t in q]
     dk = [torch.empty_like(t) for t in k]
     dv = [torch.empty_like(t) for t in v]

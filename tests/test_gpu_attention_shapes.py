@@ -1,5 +1,7 @@
 """GPU parity of the fused attention kernels beyond the golden fixtures' shapes: every head
-size the kernels support (16 / 32 / 64), frame counts that are not multiples of the 64-row
+size the kernels are built for (16 / 32 / 64) and the head sizes between them (zero-padded to
+the next kernel size, ops._padded_hd: the reference's modules take any d_model / num_heads),
+frame counts that are not multiples of the 64-row
 blocks, cross attention with Tq != Tk, hd 32 beyond one 256-key block (the fused key-block
 backward), all three mask kinds with ragged and fully padded clips — the drop-in modules against the CPU oracle (oracle/sca_oracle.py:attention), forward
 and all gradients within the north-star 1e-3.
@@ -31,6 +33,12 @@ CASES = [  # kind, B, Tq, Tk, d, H
     ("causal", 2, 520, 520, 64, 2),   # key blocks see only the queries after their first key
     ("cross", 2, 300, 530, 64, 2),    # Tk > 256, Tq != Tk
     ("causal", 1, 1024, 1024, 512, 16),  # BASELINE config 5's attention shape
+    # head sizes between the kernel sizes: zero-padded heads
+    ("self", 2, 70, 70, 48, 6),       # hd 8 -> 16
+    ("causal", 2, 90, 90, 48, 4),     # hd 12 -> 16
+    ("causal", 2, 64, 64, 36, 6),     # hd 6 -> 16
+    ("cross", 2, 40, 65, 72, 3),      # hd 24 -> 32
+    ("self", 2, 50, 50, 120, 3),      # hd 40 -> 64
 ]
 
 
@@ -42,7 +50,8 @@ def test_attention_shapes_vs_oracle(kind, B, Tq, Tk, d, H, fused):
     from scattennet_amd import _lib as L
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    if not fused and d // H not in (16, 32):
+    from scattennet_amd import ops
+    if not fused and ops._padded_hd(d // H) not in (16, 32):
         pytest.skip("the fused backward only exists for hd 16 and 32")
     L.lib().sca_attn_bwd_fused(fused)
     try:
