@@ -666,7 +666,11 @@ constexpr int FB_TS = 20;  // row stride of the 16x16 dS transposition tile (16 
 constexpr int FB_NB = 1, FB_OCC = 2;
 
 template <bool CAUSAL, bool DROP>
+#ifndef SCA_CRIT_PRIO
+#define SCA_CRIT_PRIO 2
+#endif
 __global__ __launch_bounds__(256, FB_OCC) void attn_bwd_fused_kernel(const BwdArgs a) {
+  if constexpr (SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);  // gemm.hip: critical chain
   constexpr int HD = 16, NS = 4;
   __shared__ __attribute__((aligned(16))) float Qs[FB_NB][QB * HD];
   __shared__ __attribute__((aligned(16))) float Ds[FB_NB][QB * HD];

@@ -420,6 +420,13 @@ __global__ __launch_bounds__(C::NT) void gemm_kernel(const GemmArgs args) {
 // chunk) a multiple of 32, M and N multiples of 4, one alpha for all segments of a
 // problem (applied to the accumulator).  Rows / columns past M, N are clamped on load and
 // never stored.
+// Wave priority of the backward's critical-chain kernels (input gradients, GEMM + LayerNorm
+// backward, attention backward): they share CUs with the weight-gradient launches of the side
+// stream, and s_setprio makes the SIMD arbiter issue their instructions first when both are
+// ready (the weight gradients keep priority 0 and fill the gaps)
+#ifndef SCA_CRIT_PRIO
+#define SCA_CRIT_PRIO 2
+#endif
 constexpr int GL_BM = 64, GL_BN = 64, GL_BK = 32;
 constexpr int GL_PIECE = 1024;                  // bytes per DMA wave-instruction
 constexpr int GL_OP_BYTES = GL_BM * GL_BK * 4;  // 8 KiB per operand per stage
@@ -519,6 +526,7 @@ __device__ unsigned long long g_clk[STAMP_MAX][2];  // s_memtime (shader clock) 
 
 template <int LAYOUT, int S>
 __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
+  if constexpr (LAYOUT == SCA_GEMM_NN && SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
   constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
   constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
   constexpr int STAGE = 2 * GL_OP_BYTES;
@@ -1926,6 +1934,7 @@ struct GemmLnbArgs {
 // accumulators per wave), a 32 x 512 epilogue tile, no chained GEMM.
 template <int NC>
 __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
+  if constexpr (SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
   __shared__ __attribute__((aligned(1024))) char smem[LB_SMEM];
   constexpr int VS = NC * LG_BN + 8, NROW = NC * LG_BN;
   constexpr int RED_OFF = NC == 1 ? LB_RED_OFF : LB_BM * VS * 4;  // dgamma / dbeta wave partials
