@@ -182,13 +182,14 @@ __device__ __forceinline__ TileId xcd_tile() {
 
 // ------------------------------------------------------------------------------ forward
 template <int HD, bool ADDMASK, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const FwdArgs a) {
+__global__ __launch_bounds__(256, HD <= 64 ? 2 : 1) void attn_fwd_kernel(const FwdArgs a) {
   constexpr int NS = HD / 4;   // MFMA k-steps over the head dim
   constexpr int ND = HD / 16;  // 16-wide output d-blocks
   constexpr int RV = Blk<HD>::RV;
-  __shared__ __attribute__((aligned(16))) float Ks[2][KB * HD];
-  __shared__ __attribute__((aligned(16))) float Vt[2][HD * KB];
-  __shared__ __attribute__((aligned(16))) float Ka[2][KB];
+  constexpr int NB = HD <= 64 ? 2 : 1;  // LDS buffers per image (hd 128: single, see commit)
+  __shared__ __attribute__((aligned(16))) float Ks[NB][KB * HD];
+  __shared__ __attribute__((aligned(16))) float Vt[NB][HD * KB];
+  __shared__ __attribute__((aligned(16))) float Ka[NB][KB];
 
   const TileId tid = xcd_tile();
   const sca_attn_fwd_problem& P = a.p[tid.z];
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const FwdArgs a) {
 
   auto step = [&](auto diag_c, int blk) {
     constexpr bool DIAG = decltype(diag_c)::value;
-    const int kb = blk * KB, buf = blk & 1;
+    const int kb = blk * KB, buf = NB == 2 ? (blk & 1) : 0;
     const bool more = blk + 1 < nblk;
     float sv[4][4];
     // the four key tiles' S chains are interleaved k-step by k-step: independent
@@ -326,8 +327,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const FwdArgs a) {
         for (int r = 0; r < 4; ++r) o[d] = mfma16(vv[r], sv[t][r], o[d]);
       }
     }
-    if (more) commit(buf ^ 1);
-    __syncthreads();
+    if constexpr (NB == 2) {
+      if (more) commit(buf ^ 1);
+      __syncthreads();
+    } else {  // one buffer: every wave done reading it before the next block is stored
+      __syncthreads();
+      if (more) {
+        commit(0);
+        __syncthreads();
+      }
+    }
   };
   for (int blk = 0; blk + (CAUSAL ? 1 : 0) < nblk; ++blk) step(FullStep{}, blk);
   if (CAUSAL) step(DiagStep{}, nblk - 1);
@@ -354,10 +363,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
   constexpr int NS = HD / 4;
   constexpr int ND = HD / 16;
   constexpr int RV = Blk<HD>::RV;
-  __shared__ __attribute__((aligned(16))) float Ks[2][KB * HD];
-  __shared__ __attribute__((aligned(16))) float Vs[2][KB * HD];
-  __shared__ __attribute__((aligned(16))) float Kt[2][HD * KB];
-  __shared__ __attribute__((aligned(16))) float Ka[2][KB];
+  constexpr int NB = HD <= 64 ? 2 : 1;  // hd 128: one buffer per image (96 KB of LDS)
+  __shared__ __attribute__((aligned(16))) float Ks[NB][KB * HD];
+  __shared__ __attribute__((aligned(16))) float Vs[NB][KB * HD];
+  __shared__ __attribute__((aligned(16))) float Kt[NB][HD * KB];
+  __shared__ __attribute__((aligned(16))) float Ka[NB][KB];
 
   const TileId tid = xcd_tile();
   const sca_attn_bwd_problem& P = a.p[tid.z];
@@ -432,7 +442,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
 
   auto step = [&](auto diag_c, int blk) {
     constexpr bool DIAG = decltype(diag_c)::value;
-    const int kb = blk * KB, buf = blk & 1;
+    const int kb = blk * KB, buf = NB == 2 ? (blk & 1) : 0;
     const bool more = blk + 1 < nblk;
     if (more) prefetch(kb + KB);
 #pragma unroll
@@ -470,8 +480,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const BwdArgs a) {
         for (int r = 0; r < 4; ++r) dq[d] = mfma16(kt[r], ds[r], dq[d]);
       }
     }
-    if (more) commit(buf ^ 1);
-    __syncthreads();
+    if constexpr (NB == 2) {
+      if (more) commit(buf ^ 1);
+      __syncthreads();
+    } else {  // one buffer: every wave done reading it before the next block is stored
+      __syncthreads();
+      if (more) {
+        commit(0);
+        __syncthreads();
+      }
+    }
   };
   for (int blk = 0; blk + (CAUSAL ? 1 : 0) < nblk; ++blk) step(FullStep{}, blk);
   if (CAUSAL) step(DiagStep{}, nblk - 1);
@@ -490,11 +508,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
   constexpr int NS = HD / 4;
   constexpr int ND = HD / 16;
   constexpr int RV = Blk<HD>::RV;
-  __shared__ __attribute__((aligned(16))) float Qs[2][QB * HD];
-  __shared__ __attribute__((aligned(16))) float Ds[2][QB * HD];
-  __shared__ __attribute__((aligned(16))) float Qt[2][HD * QB];
-  __shared__ __attribute__((aligned(16))) float Dt[2][HD * QB];
-  __shared__ __attribute__((aligned(16))) float Sm[2][QB], Sl[2][QB], Sd[2][QB];
+  constexpr int NB = HD <= 64 ? 2 : 1;  // hd 128: one buffer per image (128 KB of LDS)
+  __shared__ __attribute__((aligned(16))) float Qs[NB][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Ds[NB][QB * HD];
+  __shared__ __attribute__((aligned(16))) float Qt[NB][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Dt[NB][HD * QB];
+  __shared__ __attribute__((aligned(16))) float Sm[NB][QB], Sl[NB][QB], Sd[NB][QB];
 
   const TileId tid = xcd_tile();
   const sca_attn_bwd_problem& P = a.p[tid.z];
@@ -570,7 +589,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
 
   auto step = [&](auto diag_c, int blk) {
     constexpr bool DIAG = decltype(diag_c)::value;
-    const int qb = qbeg + blk * QB, buf = blk & 1;
+    const int qb = qbeg + blk * QB, buf = NB == 2 ? (blk & 1) : 0;
     const bool more = blk + 1 < nblk;
     if (more) prefetch(qb + QB);
 #pragma unroll
@@ -622,8 +641,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const BwdArgs a) {
         }
       }
     }
-    if (more) commit(buf ^ 1);
-    __syncthreads();
+    if constexpr (NB == 2) {
+      if (more) commit(buf ^ 1);
+      __syncthreads();
+    } else {  // one buffer: every wave done reading it before the next block is stored
+      __syncthreads();
+      if (more) {
+        commit(0);
+        __syncthreads();
+      }
+    }
   };
   int blk = 0;
   if (CAUSAL) step(DiagStep{}, blk++);
@@ -1122,7 +1149,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const BwdArgs a) {
 template <typename Args>
 int check_common(const Args& a, int hd, int nprob) {
   if (nprob < 1 || nprob > SCA_ATTN_MAX_PROBLEMS || a.B < 1 || a.H < 1 || a.Tq < 1 || a.Tk < 1) return 1;
-  if (hd != 16 && hd != 32 && hd != 64) return 2;
+  if (hd != 16 && hd != 32 && hd != 64 && hd != 128) return 2;
   if ((a.ldq & 3) || (a.ldk & 3) || (a.ldv & 3) || (a.ldo & 3)) return 3;
   if (a.ldq < a.H * hd || a.ldk < a.H * hd || a.ldv < a.H * hd || a.ldo < a.H * hd) return 3;
   if (a.causal && a.Tq != a.Tk) return 4;
@@ -1197,7 +1224,7 @@ extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B,
   a.drop_off = sca_drop_offset_ptr();
   const int err = check_common(a, hd, nprob);
   if (err) {
-    sca_set_error(err == 2 ? "sca_attn_fwd: head_dim must be 16, 32 or 64"
+    sca_set_error(err == 2 ? "sca_attn_fwd: head_dim must be 16, 32, 64 or 128"
                            : "sca_attn_fwd: bad shape / leading dimension / causal with Tq != Tk");
     return SCA_ERR_ARG;
   }
@@ -1228,7 +1255,8 @@ extern "C" int sca_attn_fwd(int nprob, const sca_attn_fwd_problem* probs, int B,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hd == 16) am ? launch_fwd<16, true>(a, grid, st, drop) : launch_fwd<16, false>(a, grid, st, drop);
   else if (hd == 32) am ? launch_fwd<32, true>(a, grid, st, drop) : launch_fwd<32, false>(a, grid, st, drop);
-  else am ? launch_fwd<64, true>(a, grid, st, drop) : launch_fwd<64, false>(a, grid, st, drop);
+  else if (hd == 64) am ? launch_fwd<64, true>(a, grid, st, drop) : launch_fwd<64, false>(a, grid, st, drop);
+  else am ? launch_fwd<128, true>(a, grid, st, drop) : launch_fwd<128, false>(a, grid, st, drop);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_attn_fwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
@@ -1241,7 +1269,7 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
   a.drop_off = sca_drop_offset_ptr();
   const int err = check_common(a, hd, nprob);
   if (err) {
-    sca_set_error(err == 2 ? "sca_attn_bwd: head_dim must be 16, 32 or 64"
+    sca_set_error(err == 2 ? "sca_attn_bwd: head_dim must be 16, 32, 64 or 128"
                            : "sca_attn_bwd: bad shape / leading dimension / causal with Tq != Tk");
     return SCA_ERR_ARG;
   }
@@ -1277,7 +1305,8 @@ extern "C" int sca_attn_bwd(int nprob, const sca_attn_bwd_problem* probs, int B,
   dim3 gq(causal ? (nqb + 1) / 2 : nqb, B * H, nprob), gk(causal ? (nkb + 1) / 2 : nkb, B * H, nprob);
   if (hd == 16) am ? launch_bwd<16, true>(a, gq, gk, st, drop) : launch_bwd<16, false>(a, gq, gk, st, drop);
   else if (hd == 32) am ? launch_bwd<32, true>(a, gq, gk, st, drop) : launch_bwd<32, false>(a, gq, gk, st, drop);
-  else am ? launch_bwd<64, true>(a, gq, gk, st, drop) : launch_bwd<64, false>(a, gq, gk, st, drop);
+  else if (hd == 64) am ? launch_bwd<64, true>(a, gq, gk, st, drop) : launch_bwd<64, false>(a, gq, gk, st, drop);
+  else am ? launch_bwd<128, true>(a, gq, gk, st, drop) : launch_bwd<128, false>(a, gq, gk, st, drop);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_attn_bwd: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }

@@ -995,11 +995,11 @@ def _mask_heads(add_mask):
     return add_mask.shape[1] if add_mask is not None and add_mask.dim() == 4 else 1
 
 
-_KERNEL_HD = (16, 32, 64)  # head sizes the attention kernels are built for
+_KERNEL_HD = (16, 32, 64, 128)  # head sizes the attention kernels are built for
 
 
 def _padded_hd(hd):
-    """Kernel head size for a module head size: hd itself, or the next kernel size when the
+    """Kernel head size for a module head size (<= 128): hd itself, or the next kernel size when the
     heads are zero-padded (exact: zero q / k columns add nothing to a score, zero v columns
     give zero output columns and the padded gradient columns are dropped)."""
     for k in _KERNEL_HD:

@@ -1,5 +1,5 @@
 """GPU parity of the fused attention kernels beyond the golden fixtures' shapes: every head
-size the kernels are built for (16 / 32 / 64) and the head sizes between them (zero-padded to
+size the kernels are built for (16 / 32 / 64 / 128) and the head sizes between them (zero-padded to
 the next kernel size, ops._padded_hd: the reference's modules take any d_model / num_heads),
 frame counts that are not multiples of the 64-row
 blocks, cross attention with Tq != Tk, hd 32 beyond one 256-key block (the fused key-block
@@ -39,6 +39,12 @@ CASES = [  # kind, B, Tq, Tk, d, H
     ("causal", 2, 64, 64, 36, 6),     # hd 6 -> 16
     ("cross", 2, 40, 65, 72, 3),      # hd 24 -> 32
     ("self", 2, 50, 50, 120, 3),      # hd 40 -> 64
+    # hd 128 (single-buffered LDS images) and sizes padded to it
+    ("self", 2, 100, 100, 256, 2),    # hd 128
+    ("causal", 2, 130, 130, 256, 2),  # hd 128, partial diagonal block
+    ("cross", 2, 40, 90, 384, 3),     # hd 128, Tq != Tk
+    ("self", 2, 50, 50, 192, 2),      # hd 96 -> 128
+    ("causal", 2, 70, 70, 160, 2),    # hd 80 -> 128
 ]
 
 
