@@ -45,6 +45,10 @@ CASES = [  # kind, B, Tq, Tk, d, H
     ("cross", 2, 40, 90, 384, 3),     # hd 128, Tq != Tk
     ("self", 2, 50, 50, 192, 2),      # hd 96 -> 128
     ("causal", 2, 70, 70, 160, 2),    # hd 80 -> 128
+    # d_model not a multiple of 4 (element-wise GEMM loads; heads padded to 16)
+    ("self", 2, 40, 40, 30, 5),       # hd 6
+    ("cross", 2, 30, 50, 42, 3),      # hd 14
+    ("causal", 2, 33, 33, 21, 3),     # hd 7
 ]
 
 

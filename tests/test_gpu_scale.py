@@ -223,3 +223,11 @@ def test_full_encoder_vs_oracle(monkeypatch, wname):
     for k, prm in named.items():  # parameters the reference never trains (long shortcuts)
         if k not in grads:
             assert prm.grad is None, k
+
+
+@pytest.mark.parametrize("d,H", [(30, 5), (200, 8)])
+def test_odd_widths_stream_vs_oracle(d, H):
+    """A whole SCA stream (mapping, embedding LN, self / causal / merge layers with FFNs) at a
+    d_model that is not a multiple of 4 (element-wise GEMM loads, scalar LayerNorm rows) and
+    at a head size between the kernel sizes (hd 6 and 25, zero-padded heads)."""
+    _run(f"d{d}_H{H}", dict(B=3, T=45, K_all=9, groups=[9], d=d, H=H, L=2, residual=False, maxpos=64))
