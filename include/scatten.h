@@ -75,7 +75,8 @@ typedef struct {
   const float* A;
   const float* B;
   int lda, ldb;
-  int K;       /* reduction length of this segment (multiple of 4 for NT / NN; any for TN) */
+  int K;       /* reduction length of this segment (any: K, lda, ldb not multiples of 4 or
+                  operands not 16-byte aligned take the element-wise load form) */
   float alpha; /* scales A on load: alpha=0.5 reproduces v_proj(kv/2) exactly */
 } sca_gemm_seg;
 

@@ -1021,7 +1021,7 @@ def _unpad_heads(ts, H, hd, hdp):
 
 def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
     """drop: None or (p, seeds) — attention-probability dropout, one seed per problem.
-    Head sizes other than 16 / 32 / 64 run zero-padded to the next kernel size."""
+    Head sizes other than 16 / 32 / 64 / 128 run zero-padded to the next kernel size."""
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
