@@ -127,7 +127,10 @@ def sca_grouped(scas, xs, ys, attention_mask):
     p = drop_p(scas)
     if attention_mask is None:
         raise AttributeError("'NoneType' object has no attribute 'size'")  # reference: mask.size()
-    x_self = scas[0].x_self
+    if len({bool(m.x_self) for m in scas}) > 1:
+        # one grouped launch serves every stream: their self / causal inputs must agree
+        raise ValueError("sca_grouped: the grouped SCA stacks mix self_attn_x=True and False")
+    x_self = scas[0].x_self  # keypoint_module.py:154-159
     se, ce = (xs, ys) if x_self else (ys, xs)
     tabs = [m.self_pos_embed for m in scas] + [m.causal_pos_embed for m in scas]
     norms = [m.first_self_norm for m in scas] + [m.first_causal_norm for m in scas]

@@ -95,6 +95,7 @@ def build_streams(w, device, seed=0, init="reference"):
     from .keypoint_module import KeypointModule, KeypointStreams
     torch.manual_seed(seed)
     cfg = model_cfg(w["d"], w["H"], w["L"], maxpos=w["maxpos"])
+    cfg.update(w.get("cfg_over", {}))  # e.g. {"self_attn_x": False}
     mods = [KeypointModule(g, w["T"], cfg) for g in split_groups(w["groups"])]
     streams = KeypointStreams(mods, with_residual=w["residual"])
     if init == "reference":

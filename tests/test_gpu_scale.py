@@ -17,7 +17,7 @@ PARITY_TOL = 1e-3  # north_star: within 1e-3 relative fp32
 pytestmark = pytest.mark.gpu
 
 
-def _run(name, w, streams_used=None):
+def _run(name, w, streams_used=None, cfg_over=None):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     torch.set_num_threads(min(16, torch.get_num_threads()))
@@ -25,6 +25,8 @@ def _run(name, w, streams_used=None):
     w = dict(w)
     if streams_used is not None:
         w["groups"] = w["groups"][:streams_used]
+    if cfg_over:
+        w["cfg_over"] = dict(cfg_over)
     model = W.build_streams(w, dev, seed=3, init="random")
     kp, mask, gout = W.synthetic_batch(w, dev, seed=5, ragged=True)
     outs = model(kp, mask)
@@ -32,6 +34,7 @@ def _run(name, w, streams_used=None):
     torch.cuda.synchronize()
 
     cfg = W.model_cfg(w["d"], w["H"], w["L"], maxpos=w["maxpos"])
+    cfg.update(w.get("cfg_over", {}))
     groups = W.split_groups(w["groups"])
     for g, mod in enumerate(model.streams):
         p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in mod.state_dict().items()}
@@ -59,6 +62,85 @@ def test_cfg5_long_sequence_vs_oracle(fuse512, monkeypatch):
     from scattennet_amd import ops
     monkeypatch.setattr(ops, "_FUSE_LN512", fuse512)
     _run("cfg5", W.WORKLOADS["cfg5"], streams_used=1)
+
+
+def test_cfg5_four_grouped_streams_vs_oracle():
+    """Config 5 as the bench runs it — the four streams (23/68/21/21 joints) in grouped
+    launches at T = 1024, d = 512, hd 32 — at B = 2 (ragged: T and T - 37 valid frames)."""
+    _run("cfg5x4", dict(W.WORKLOADS["cfg5"], B=2))
+
+
+def test_self_attn_x_false_vs_oracle():
+    """cfg["self_attn_x"] = False sends the y coordinates through the self (unmasked) stack
+    and x through the causal one (keypoint_module.py:154-159); two grouped streams."""
+    _run("x_self_false", dict(B=3, T=48, K_all=15, groups=[6, 9], d=64, H=4, L=2, residual=False, maxpos=64),
+         cfg_over={"self_attn_x": False})
+
+
+def test_mixed_self_attn_x_group_raises():
+    """One grouped launch cannot serve streams with different self_attn_x."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    w = dict(B=2, T=16, K_all=8, groups=[4, 4], d=32, H=2, L=1, residual=False, maxpos=32)
+    model = W.build_streams(w, dev, seed=1, init="random")
+    model.streams[1].sca.x_self = False
+    kp, mask, _ = W.synthetic_batch(w, dev, seed=2)
+    with pytest.raises(ValueError, match="self_attn_x"):
+        model(kp, mask)
+
+
+def test_cfg1_four_self_layers_vs_oracle():
+    """BASELINE config 1 as SURVEY §8(d) defines it (x-stream, 4 self layers; B=2 T=64 K=27
+    d=64 H=4) through the HIP drop-ins against oracle.x_stream (which the reference's own
+    L = 2 fixture, xstream_cfg1.npz, pins)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import scattennet_amd as S
+    from scattennet_amd.layers import coordinate_mapping_grouped, pos_embed_layernorm_grouped
+    from torch import nn
+    dev = torch.device("cuda:0")
+    w = W.WORKLOADS["cfg1"]
+    cfg = W.model_cfg(w["d"], w["H"], w["L"], maxpos=w["maxpos"])
+    assert cfg["attn_layers"] == 4
+
+    class XStream(nn.Module):  # KeypointModule key names, x-stream only
+        def __init__(self):
+            super().__init__()
+            self.coordinate_mapping = S.CoordinateMapping(w["K_all"], cfg["d_model"])
+            self.sca = nn.Module()
+            self.sca.self_attn_layers = nn.ModuleList([S.CoordinateAttention(cfg, "self_attn")
+                                                       for _ in range(cfg["attn_layers"])])
+            self.sca.first_self_norm = nn.LayerNorm(cfg["d_model"])
+            self.sca.self_pos_embed = S.LearningPositionEmbedding(cfg["max_position_embeddings"], cfg["d_model"])
+
+        def forward(self, keypoints, mask):
+            cm = self.coordinate_mapping
+            xe, _ = coordinate_mapping_grouped([cm], keypoints, [cm.joint_index(keypoints.device)])
+            s = pos_embed_layernorm_grouped([self.sca.self_pos_embed], [self.sca.first_self_norm], xe)[0]
+            m = S.create_attention_mask(mask, s.dtype)
+            for layer in self.sca.self_attn_layers:
+                s = layer(s, m)
+            return s
+
+    torch.manual_seed(0)
+    mod = XStream()
+    W.randomize(mod, 9)
+    mod = mod.to(dev)
+    kp, mask, _ = W.synthetic_batch(w, dev, seed=4, ragged=True)
+    out = mod(kp, mask)
+    gout = torch.randn(out.shape, generator=torch.Generator().manual_seed(2)).to(dev)
+    out.backward(gout)
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in mod.state_dict().items()}
+    ref = O.x_stream(p, "", kp.cpu(), mask.cpu(), cfg)
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * gout.cpu()).sum().backward()
+    grads = {k: v.grad for k, v in p.items() if v.grad is not None}
+    gscale = max(float(t.abs().max()) for t in grads.values())
+    named = dict(mod.named_parameters())
+    assert len(grads) > 4 * 10
+    for k, gr in grads.items():
+        assert close(named[k].grad.cpu(), gr, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), gr))
 
 
 def _encoder_oracle(enc, cfg, kp, mask, gout):
