@@ -214,9 +214,17 @@ typedef struct {
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);
 int sca_gemm_lnb_blocks(int M);
 
-/* Tuning knob: force the workgroup tile of one layout (0 = built-in heuristic,
- * 1 = 64x64, 2 = 128x64, 3 = 64x128, 4 = 128x128).  Process-global; not thread-safe.   */
+/* Tuning knob: force the kernel variant of one layout for every later sca_gemm* call
+ * (0 = built-in heuristic; 1 / 5 / 7 register-staged 64x64 / single-buffered 64x64 /
+ * 128x64 8 waves; 20 / 21 / 22 LDS-DMA 64x64 with a 3- / 2- / 4-stage ring; 36 / 37, TN
+ * only: the k-split weight-gradient kernel with a 3- / 4-stage ring — every variant computes
+ * the full result).  Any other id: SCA_ERR_ARG, nothing changed.  Process-global.          */
 int sca_gemm_tile_override(int layout, int tile);
+/* sca_gemm with the kernel variant chosen for this call only (ids as above, 0 = the override
+ * or heuristic; an invalid id is SCA_ERR_ARG): split-K slabs combined in-launch when
+ * `counters` is given and the variant can (sca_gemm_splitk_fused), else the two-launch form. */
+int sca_gemm_variant(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                     unsigned* counters, int variant, void* stream);
 
 /* Fused masked attention over (B, T, H*hd) row-major activations (head h at columns
  * h*hd .. h*hd+hd-1, row stride ld*).  Scores use q as given (the projection already

@@ -121,6 +121,7 @@ EXPORTS = {
     "sca_gemm_tile_override": ([c_int, c_int], c_int),
     "sca_gemm_splitk_counters": ([c_int, c_int, c_int], c_long),
     "sca_gemm_splitk_fused": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
+    "sca_gemm_variant": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "sca_gemm_ln_rows": ([c_int, c_int, c_int], c_int),
     "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
@@ -181,10 +182,6 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest
-        # tuning knob: SCA_GEMM_TILES="nt,nn,tn" forces a tile config per layout (0 = heuristic)
-        for layout, t in enumerate(os.environ.get("SCA_GEMM_TILES", "").split(",")):
-            if t.strip():
-                L.sca_gemm_tile_override(layout, int(t))
         _lib = L
     return _lib
 
@@ -193,17 +190,12 @@ class HipOpError(RuntimeError):
     pass
 
 
-POST_LAUNCH = None  # ops installs a hook run after every successful C-ABI launch
-
-
 def check(rc, what):
     if rc != 0:
         msg = lib().sca_last_error().decode()
         if rc == 1:
             raise ValueError(f"{what}: {msg}")
         raise HipOpError(f"{what} failed ({rc}): {msg}")
-    if POST_LAUNCH is not None:
-        POST_LAUNCH()
 
 
 def stream_handle():
@@ -222,17 +214,24 @@ def require_device(*tensors):
 
 
 def source_digest():
-    """sha256 (first 16 hex digits) of the HIP library's sources (csrc/*.hip, *.h, *.cpp and
-    include/scatten.h): identifies the build a committed rocprofv3 profile was measured on
-    (bench.py reports the profile's figures only for a matching build)."""
+    """sha256 (first 16 hex digits) of everything that decides which kernels a bench step
+    runs and how: the HIP library's sources (csrc/*.hip, *.h, *.cpp, include/scatten.h), the
+    Python dispatch that picks variants, tiles and split-K (scattennet_amd/*.py, bench.py) and
+    the SCA_* environment settings in force (bench.py's own
+    DEBUG_HIP_* default is part of its source).  Identifies the build a committed
+    rocprofv3 profile was measured on (bench.py reports the profile's figures only for a
+    matching digest)."""
     import glob
     import hashlib
     h = hashlib.sha256()
     root = os.path.dirname(_HERE)
     files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h")) +
-                   glob.glob(os.path.join(_HERE, "csrc", "*.cpp")) + [os.path.join(root, "include", "scatten.h")])
+                   glob.glob(os.path.join(_HERE, "csrc", "*.cpp")) + [os.path.join(root, "include", "scatten.h")] +
+                   glob.glob(os.path.join(_HERE, "*.py")) + [os.path.join(root, "bench.py")])
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
+    env = sorted((k, v) for k, v in os.environ.items() if k.startswith("SCA_") and k != "SCA_LIB_PATH")
+    h.update(repr(env).encode())
     return h.hexdigest()[:16]

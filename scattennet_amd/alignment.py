@@ -26,8 +26,8 @@ from .ops import _prob, _seg, gemm
 
 # split-K of the per-step recurrent GEMMs (M = B rows only): forward K = H, backward K = 4H
 # would otherwise run on N/64 workgroups per direction
-_SPLITK_FWD = int(__import__("os").environ.get("SCA_LSTM_SPLITK_FWD", "8"))
-_SPLITK_BWD = int(__import__("os").environ.get("SCA_LSTM_SPLITK_BWD", "16"))
+_SPLITK_FWD = 8
+_SPLITK_BWD = 16
 
 
 def _stepper(template, a_step, r_step):

@@ -90,7 +90,7 @@ def _resolve_mask(mask, causal, B, Tq, Tk, device, H=1):
     raise TypeError(f"unsupported attention_mask type {type(mask)}")
 
 
-def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln=None, nxt=None, kvacc=None):
+def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln=None, nxt=None):
     """Run G attention operators of the same shape in lock-step (one launch per stage).
 
     kind: "self" | "causal" | "cross".  Returns dropout(out_proj(attn), drop_p), plus the
@@ -98,9 +98,7 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
     residual and dropout ride in the out-projection epilogue).  `ln` (G nn.LayerNorms): the
     enclosing block's LayerNorm applied to that result — fused into the out-projection
     launch (sca_gemm_ln) when d_model = 256, a separate LayerNorm launch otherwise.  `nxt`
-    (ops.NextProjections): the next op's projections, chained into that launch when fused.
-    `kvacc` (cross only): (ops.KvGradAccumulator, index) — the key/value input's gradient
-    accumulated over a chain of blocks sharing it (index 0 = the chain's first block)."""
+    (ops.NextProjections): the next op's projections, chained into that launch when fused."""
     G = len(attns)
     a0 = attns[0]
     # attention-probability dropout (attention.py:67-69 / 119-121 / 173-175): F.dropout(p,
@@ -129,7 +127,7 @@ def attention_grouped(attns, kind, hidden, kv, mask, resid=False, drop_p=0.0, ln
         ts += [n.weight for n in ln] + [n.bias for n in ln]
     out = list(library.attention_block_apply(G, kind, a0.num_heads, a0.scaling, plus_one, key_valid, add_mask,
                                         bool(resid), float(drop_p), float(ln[0].eps) if fuse else None,
-                                        nxt if fuse else None, kvacc if kind == "cross" else None, attn_p, *ts))
+                                        nxt if fuse else None, attn_p, *ts))
     if ln is not None and not fuse:
         from .layers import layernorm_grouped
         out = layernorm_grouped(ln, out)

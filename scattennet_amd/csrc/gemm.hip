@@ -31,9 +31,6 @@ struct GemmArgs {
   sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
   int splitk;
   float* ws;
-  int nprob;                                    // persistent kernel only:
-  int tile_prefix[SCA_GEMM_MAX_PROBLEMS + 1];  // cumulative output tiles (x splitk) per problem
-  int tiles_n[SCA_GEMM_MAX_PROBLEMS];           // column tiles per problem
   const unsigned long long* drop_off;           // dropout step counter (sca_dropout_offset)
   long slab_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first partial slab in ws
   long bias_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first bias partial row in ws
@@ -727,9 +724,8 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
 constexpr int TNK_PLD = 68;  // partial-tile row stride (floats): 16-B shift per row
 constexpr int TNK_RED = 4 * 64 * TNK_PLD * 4 + 4 * 64 * 4;  // 4 partial tiles + 4 bias partial rows
 
-// SUB: K slices per ring stage (one wait + barrier per SUB x 32 k rows); PF (SUB = 1): the
-// fragments of slice t+1 are read from LDS during slice t's MFMAs (register double buffer)
-template <int S, int SUB, bool PF = false, int NODMA = 0>
+// SUB: K slices per ring stage (one wait + barrier per SUB x 32 k rows)
+template <int S, int SUB>
 __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   constexpr int SLICE = 2 * GL_OP_BYTES;
   constexpr int STAGE = SUB * SLICE;
@@ -811,61 +807,6 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto frags = [&](const char* stage, f32x4 (&a)[2], f32x4 (&b)[2]) {
-    const float* As = reinterpret_cast<const float*>(stage);
-    const float* Bs = As + GL_BM * GL_BK;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = 4 * (2 * wave + h) + g;  // image row: this wave's k quarter of the slice
-      a[h] = ld4(As + k * GL_BM + 4 * c);
-      b[h] = ld4(Bs + k * GL_BN + 4 * c);
-    }
-  };
-  auto mma = [&](const f32x4 (&a)[2], const f32x4 (&b)[2]) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (do_bias) bs4 += a[h];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[h][i], b[h][j], acc[i][j]);
-    }
-  };
-  if constexpr (PF) {
-    static_assert(SUB == 1 && S >= 2, "PF: one slice per stage");
-    // iteration t: slice t+1 landed (every wave also holds slice t's fragments: lgkmcnt(0)),
-    // barrier, DMA slice t+S into slice t's stage, read slice t+1's fragments, MFMAs of t
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if (i < total) dma(i, i);
-    f32x4 ca[2], cb[2], na[2], nb[2];
-    if (total > 0) {
-      if (total >= S) gl_wait_vm<4 * (S - 1)>();  // slice 0 landed (slices 1 .. S-1 may fly)
-      else gl_wait_vm<0>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      frags(smem, ca, cb);
-    }
-    for (int t = 0; t < total; ++t) {
-      if (t + 1 < total) {
-        // slice t+1 landed: the slices issued after it (up to t+S-1) may still fly
-        const int younger = min(total - 1, t + S - 1) - (t + 1);
-        if (younger >= S - 2) gl_wait_vm<4 * (S - 2)>();
-        else gl_wait_vm<0>();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): slice t's fragments are in registers
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (!NODMA && t + S < total) dma(t + S, t % S);
-        frags(smem + ((t + 1) % S) * STAGE, na, nb);
-      }
-      mma(ca, cb);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        ca[h] = na[h];
-        cb[h] = nb[h];
-      }
-    }
-  } else {
 #pragma unroll
   for (int i = 0; i < S - 1; ++i)
     if (i < nst) dma_stage(i, i);
@@ -875,9 +816,9 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   for (int u = 0; u < nst; ++u) {
     if (u + S - 2 < nst && (whole || u + S - 2 < nst - 1)) gl_wait_vm<4 * SUB * (S - 2)>();
     else gl_wait_vm<0>();
-    if (NODMA < 2) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if ((NODMA == 0 || NODMA == 3) && u + S - 1 < nst) dma_stage(u + S - 1, (u + S - 1) % S);  // NODMA: probes
+    if (u + S - 1 < nst) dma_stage(u + S - 1, (u + S - 1) % S);
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
       if (u * SUB + q >= total) break;
@@ -893,17 +834,12 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (do_bias) bs4 += a[h];
-        if (NODMA == 3) {  // memory-pipeline probe: consume the fragments without MFMAs
-          acc[0][0] += a[h] + b[h];
-          continue;
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[h][i], b[h][j], acc[i][j]);
       }
     }
-  }
   }
 
   // the 4 waves' partial tiles (and bias rows) through LDS, summed in fixed order per quadrant
@@ -986,523 +922,6 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
     return;
   }
   epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
-}
-
-// ------------------------------------------------------------------------------ LDS-DMA, 8 waves
-// gemm_glds_kernel's 64x64 tile with TWO 4-wave groups that split the K-slices of the tile
-// between them (group g computes slices g, g+2, ...; the ring stage holds one slice per
-// group, each exactly gemm_glds_kernel's slice image, DMA'd by its own group); the groups'
-// accumulators are summed through LDS before the epilogue.  For long-K launches with few
-// tiles (the weight gradients: 16 x (256 x 256) at K = B*T = 2048 are 256 tiles, one per CU)
-// it gives two waves per SIMD without split-K slabs or a reduce launch.
-template <int LAYOUT, int S>
-__global__ __launch_bounds__(512) void gemm_glds2_kernel(const GemmArgs args) {
-  constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
-  constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
-  constexpr int SLICE = 2 * GL_OP_BYTES;  // one group's slice image (A then B)
-  constexpr int STAGE = 2 * SLICE;
-  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
-
-  const unsigned gx = gridDim.x, gy = gridDim.y;
-  const unsigned nwg = gx * gy * gridDim.z;
-  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
-
-  const int splitk = args.splitk;
-  const int pid = bz / splitk;
-  const int ks = bz % splitk;
-  const sca_gemm_problem& P = args.p[pid];
-  const int m0 = by * GL_BM, n0 = bx * GL_BN;
-  if (m0 >= P.M || n0 >= P.N) return;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = wave >> 2, w4 = wave & 3;  // K-slice group, wave within the group
-  const int wm = (w4 >> 1) * 32, wn = (w4 & 1) * 32;
-
-  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
-  int total = 0;
-#pragma unroll
-  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
-    seg_kbeg[s] = seg_n[s] = 0;
-    if (s < P.nseg) {
-      int kbeg = 0, kend = P.seg[s].K;
-      if (splitk > 1) {
-        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + GL_BK - 1) / GL_BK * GL_BK;
-        kbeg = ks * chunk;
-        kend = min(P.seg[s].K, kbeg + chunk);
-      }
-      seg_kbeg[s] = kbeg;
-      seg_n[s] = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
-      total += seg_n[s];
-    }
-  }
-  const int pairs = (total + 1) / 2;  // ring stages to walk; group g owns slice 2p + g
-  int iseg = -1, tseg0 = 0, tend = 0;
-  const float* pa[2] = {nullptr, nullptr};
-  const float* pb[2] = {nullptr, nullptr};
-  long stepA = 0, stepB = 0;
-  auto dma = [&](int p, int stage) {  // this group's slice of stage p (slices issued in order)
-    const int t = 2 * p + grp;
-    if (t >= total) return;
-    while (t >= tend) {
-      ++iseg;
-      tseg0 = tend;
-      tend += seg_n[iseg];
-      const sca_gemm_seg& G = P.seg[iseg];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        pa[c] = gl_src<A_KC>(G.A, G.lda, m0, P.M, seg_kbeg[iseg], c, w4, lane);
-        pb[c] = gl_src<B_KC>(G.B, G.ldb, n0, P.N, seg_kbeg[iseg], c, w4, lane);
-      }
-      stepA = A_KC ? GL_BK : (long)GL_BK * G.lda;
-      stepB = B_KC ? GL_BK : (long)GL_BK * G.ldb;
-    }
-    const long kk = t - tseg0;
-    char* base = smem + stage * STAGE + grp * SLICE;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      gl_dma(pa[c] + kk * stepA, base + gl_dst<A_KC>(c, w4));
-      gl_dma(pb[c] + kk * stepB, base + GL_OP_BYTES + gl_dst<B_KC>(c, w4));
-    }
-  };
-
-  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && bx == 0;
-  float bsum = 0.f;
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < pairs) dma(i, i);
-  for (int p = 0; p < pairs; ++p) {
-    // each wave issued 4 DMAs per stage in which its group has a slice; S-2 younger stages
-    // may stay in flight except at the tail, where a group may have issued fewer
-    if (p + S - 2 < pairs && 2 * (p + S - 2) + 1 < total) gl_wait_vm<4 * (S - 2)>();
-    else gl_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (p + S - 1 < pairs) dma(p + S - 1, (p + S - 1) % S);
-    if (2 * p + grp < total) {
-      const char* As = smem + (p % S) * STAGE + grp * SLICE;
-      const char* Bs = As + GL_OP_BYTES;
-      if (do_bias && w4 == 0) {
-        const float* af = (const float*)As;  // TN: A image is [32 k][64 m]
-#pragma unroll 8
-        for (int k = 0; k < GL_BK; ++k) bsum += af[k * 64 + lane];
-      }
-      f32x4 fa[4], fb[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        fa[g] = gl_frag<A_KC>(As, wm, g, lane);
-        fb[g] = gl_frag<B_KC>(Bs, wn, g, lane);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
-    }
-  }
-  // group 1 hands its partial tile (and bias partial) to group 0 through the freed ring
-  __syncthreads();
-  float* X = reinterpret_cast<float*>(smem);
-  if (grp == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) X[(w4 * 16 + r) * 64 + lane] = acc[r];
-    if (w4 == 0) X[4 * 16 * 64 + lane] = bsum;
-  }
-  __syncthreads();
-  if (grp == 1) return;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] += X[(w4 * 16 + r) * 64 + lane];
-  if (w4 == 0) bsum += X[4 * 16 * 64 + lane];
-
-  const float alpha = P.seg[0].alpha;
-  const int col = lane & 31;
-  const int rowh = 4 * (lane >> 5);
-  if (do_bias && w4 == 0 && m0 + lane < P.M) {
-    if (splitk > 1)
-      args.ws[args.bias_off[pid] + (long)ks * P.M + m0 + lane] = bsum * alpha;
-    else
-      P.bias_grad[m0 + lane] = bsum * alpha * P.bias_grad_scale;
-  }
-  if (alpha != 1.f) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] *= alpha;
-  }
-  (void)col;
-  (void)rowh;
-  f32x4 rows[4];  // transposition scratch past the hand-off buffer X
-  acc_to_rows(acc, reinterpret_cast<float*>(smem + 20 * 1024) + w4 * 32 * EPI_LD, lane, rows);
-  if (splitk > 1) {
-    slab_rows(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N, rows, P.M, P.N, m0 + wm, n0 + wn, lane);
-    return;
-  }
-  epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
-}
-
-// ------------------------------------------------------------------------------ TN, large tiles
-// The weight-gradient layout dW[M = out][N = in] = alpha * sum_k A[k][m] B[k][n] (A = dY,
-// B = X, both row-major (M_red, .) with the reduction over their ROWS): both operand tiles
-// are k-major [32 k][rows] LDS images filled by LDS-DMA straight from the row-major
-// activations (lane-linear pieces, no swizzle: a half-wave's fragment read is 32 (or 64 /
-// 128) consecutive floats of one k-row — conflict-free).  Against the 64x64 / 4-wave kernel:
-//   * bigger workgroup tiles (128 x 64, 128 x 128): 21-32 FLOP per staged byte instead of 16,
-//     so half the L2 -> LDS traffic per MFMA and fewer split-K partial slabs for the same fill;
-//   * wave tiles of up to 64 x 64 read by ds_read_b64 / b128: the rows of MFMA block i are the
-//     wave's rows RM*r + i (a free row permutation, undone in the epilogue), so one 8-/16-byte
-//     read feeds RM blocks — 2-4x fewer LDS reads per MFMA than 32x32 wave tiles;
-//   * a ring of S stages with a counted vmcnt that keeps S-2 slices in flight across the
-//     slice barrier (S = 3, 4; the 64x64 kernel's 2-stage ring waits for vmcnt(0) every slice);
-//   * split-K combined in the launch as gemm_glds_kernel does (write-through slabs, arrival
-//     ticket, the last arriver sums the slabs in slice order — deterministic), except that the
-//     last arriver takes its own partial from registers instead of re-reading its slab.
-// Requirements: tn_ok (every split-K chunk a multiple of 32 rows, M and N multiples of 4, one
-// alpha per problem) and vec_ok.
-template <int BM_, int BN_, int WM_, int WN_, int S_, int LW_ = 0, bool PF_ = false>
-struct TnCfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_;
-  static constexpr bool PF = PF_;         // fragments read one slice ahead (needs S >= 3)
-  static_assert(!PF || S >= 3, "prefetch needs a 3-stage ring");
-  static constexpr int NW = WM * WN;      // compute waves
-  static constexpr int LW = LW_;          // loader waves (0: the compute waves issue the DMA)
-  static constexpr int NT = 64 * (NW + LW);
-  static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
-  static constexpr int RM = TM / 32, RN = TN / 32;  // 32x32 MFMA blocks per wave
-  static constexpr int A_BYTES = GL_BK * BM * 4, B_BYTES = GL_BK * BN * 4, STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_PC = A_BYTES / GL_PIECE, B_PC = B_BYTES / GL_PIECE;  // DMA pieces per slice
-  static constexpr int DW = LW > 0 ? LW : NW;                                   // waves issuing them
-  static constexpr int PPW = (A_PC + B_PC) / DW;                                // ... pieces each
-  static constexpr int SCR_LD = TN + 4;                                         // epilogue scratch row
-  static constexpr int SCR_BYTES = TM * SCR_LD * 4;                             // ... per wave
-  static constexpr int RING = S * STAGE, SCR = NW * SCR_BYTES;
-  static constexpr int SMEM = (RING > SCR ? RING : SCR) + 16;                   // + the ticket flag
-  static constexpr int Q = TM * TN / 256;  // float4 row pieces per lane in the epilogue
-  static_assert((A_PC + B_PC) % DW == 0, "DMA pieces must divide among the issuing waves");
-  static_assert((RM == 1 || RM == 2 || RM == 4) && (RN == 1 || RN == 2 || RN == 4), "wave tile");
-  static_assert(TN % 4 == 0 && 256 % TN == 0, "row pieces");
-  static_assert(SMEM <= 160 * 1024, "LDS");
-};
-
-// RM floats at consecutive addresses (the RM MFMA blocks' operands of one lane at one k)
-template <int R>
-__device__ __forceinline__ void tn_read(const float* p, float (&o)[R]) {
-  if constexpr (R == 1) {
-    o[0] = p[0];
-  } else if constexpr (R == 2) {
-    const float2 v = *reinterpret_cast<const float2*>(p);
-    o[0] = v.x;
-    o[1] = v.y;
-  } else {
-    const f32x4 v = ld4(p);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = v[i];
-  }
-}
-
-// epilogue_rows' per-row-piece arithmetic for one float4 of row m, columns n .. n+3
-__device__ __forceinline__ void epilogue_row4(const sca_gemm_problem& P, int m, int n, f32x4 v, const DropMask& dm) {
-  const f32x4 bias = P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 ex = {0.f, 0.f, 0.f, 0.f}, ax = ex;
-  if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
-  if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
-  if (P.epi & SCA_EPI_DGELU) ax = ld4(P.aux + (long)m * P.ldx + n);
-  f32x4 o = (v + bias) * P.post_scale;
-  if (P.epi & SCA_EPI_GELU) {
-    st4(P.aux_out + (long)m * P.ldo + n, o);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
-  }
-  if (P.epi & SCA_EPI_DROPOUT) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), o[j]);
-  }
-  if (P.epi & SCA_EPI_DGELU) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
-  }
-  st4(P.C + (long)m * P.ldc + n, o + ex);
-}
-
-template <class C>
-__global__ __launch_bounds__(C::NT) void gemm_tn_kernel(const GemmArgs args) {
-  constexpr int BM = C::BM, BN = C::BN, S = C::S, RM = C::RM, RN = C::RN, TM = C::TM, TN = C::TN;
-  constexpr int PPW = C::PPW, Q = C::Q, NW = C::NW, LW = C::LW;
-  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
-
-  const unsigned gx = gridDim.x, gy = gridDim.y;
-  const unsigned nwg = gx * gy * gridDim.z;
-  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
-  const int splitk = args.splitk;
-  const int pid = bz / splitk, ks = bz % splitk;
-  const sca_gemm_problem& P = args.p[pid];
-  const int m0 = by * BM, n0 = bx * BN;
-  if (m0 >= P.M || n0 >= P.N) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool computes = wave < NW;              // loader waves (wave >= NW) only stream the ring
-  const bool issues = LW == 0 || !computes;     // waves that issue the DMA
-  const int dwave = LW == 0 ? wave : wave - NW;  // index among the issuing waves
-  const int cw = computes ? wave : 0;
-  const int wm = (cw / C::WN) * TM, wn = (cw % C::WN) * TN;
-  const sca_gemm_seg& G = P.seg[0];
-
-  int kbeg = 0, kend = G.K;
-  if (splitk > 1) {
-    const int chunk = ((G.K + splitk - 1) / splitk + GL_BK - 1) / GL_BK * GL_BK;
-    kbeg = ks * chunk;
-    kend = min(G.K, kbeg + chunk);
-  }
-  const int total = kend > kbeg ? (kend - kbeg) / GL_BK : 0;
-
-  // the issuing wave's DMA pieces: piece q < A_PC is k-rows 256/BM*q .. of the A image, else of B
-  const float* src[PPW];
-  int dst[PPW];
-  long step[PPW];
-#pragma unroll
-  for (int c = 0; c < PPW; ++c) {
-    const int q = dwave * PPW + c;
-    const bool isA = q < C::A_PC;
-    const int rows = isA ? BM : BN, qq = isA ? q : q - C::A_PC;
-    const int kr = qq * (256 / rows) + lane / (rows / 4), col = 4 * (lane % (rows / 4));
-    const float* base = isA ? G.A : G.B;
-    const int ld = isA ? G.lda : G.ldb;
-    const int r0 = isA ? m0 : n0, nr = isA ? P.M : P.N;
-    src[c] = base + (long)(kbeg + kr) * ld + min(r0 + col, nr - 4);
-    dst[c] = (isA ? 0 : C::A_BYTES) + qq * GL_PIECE;
-    step[c] = (long)GL_BK * ld;
-  }
-  auto dma = [&](int t, int stage) {
-    char* b = smem + stage * C::STAGE;
-#pragma unroll
-    for (int c = 0; c < PPW; ++c) gl_dma(src[c] + t * step[c], b + dst[c]);
-  };
-
-  const bool do_bias = computes && P.bias_grad != nullptr && bx == 0 && wn == 0;
-  float bsum[RM];
-#pragma unroll
-  for (int i = 0; i < RM; ++i) bsum[i] = 0.f;
-  f32x16 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int r = lane & 31, h = lane >> 5;
-  if (issues) {
-#pragma unroll
-    for (int i = 0; i < S - 1; ++i)
-      if (i < total) dma(i, i);
-  }
-  // fragments of a slice in registers: [k-group g][k-step j][block]
-  using FragA = float[4][4][RM];
-  using FragB = float[4][4][RN];
-  auto read_frags = [&](int t, FragA& fa, FragB& fb) {
-    const float* As = reinterpret_cast<const float*>(smem + (t % S) * C::STAGE);
-    const float* Bs = As + GL_BK * BM;
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = 8 * g + 4 * h + j;
-        tn_read<RM>(As + k * BM + wm + RM * r, fa[g][j]);
-        tn_read<RN>(Bs + k * BN + wn + RN * r, fb[g][j]);
-      }
-  };
-  auto mfmas = [&](const FragA& fa, const FragB& fb) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < RN; ++jj) acc[i][jj] = mfma32(fa[g][j][i], fb[g][j][jj], acc[i][jj]);
-      if (do_bias) {  // colsum of dY = row sums of the A image: lane (r, h) holds rows RM r + i
-#pragma unroll
-        for (int i = 0; i < RM; ++i) bsum[i] += (fa[g][0][i] + fa[g][1][i]) + (fa[g][2][i] + fa[g][3][i]);
-      }
-    }
-  };
-  if constexpr (C::PF) {
-    // fragments one slice ahead: after the barrier that publishes slice t + 1 a compute wave
-    // issues the LDS reads of slice t + 1 and the MFMAs of slice t (its fragments already in
-    // registers), so no LDS latency sits between a barrier and the MFMAs.  The barrier of
-    // iteration t requires slices <= t + 1 landed (S - 3 younger slices in flight) and
-    // every wave done READING slices <= t, so the DMA of slice t + S - 1 may overwrite the
-    // stage of slice t - 1.
-    FragA fa0, fa1;
-    FragB fb0, fb1;
-    if (issues) {
-      if (total >= S - 1) gl_wait_vm<PPW * (S - 2)>();
-      else gl_wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (computes && total > 0) read_frags(0, fa0, fb0);
-    auto iter = [&](int t, FragA& fa_cur, FragB& fb_cur, FragA& fa_nxt, FragB& fb_nxt) {
-      if (issues) {
-        if (t + S - 2 < total) gl_wait_vm<PPW * (S - 3)>();
-        else gl_wait_vm<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
-      if (!computes) return;
-      // the current fragments' reads (issued an iteration ago) are complete: say so to the
-      // waitcnt pass, which cannot otherwise wait for them behind 16 younger LDS reads (the
-      // lgkmcnt field holds 15) and would wait for the next slice's reads before the MFMAs
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt unconstrained
-      read_frags(t + 1, fa_nxt, fb_nxt);   // past the last slice: a stale stage, never used
-      mfmas(fa_cur, fb_cur);
-    };
-    for (int t = 0; t < total; t += 2) {
-      iter(t, fa0, fb0, fa1, fb1);
-      if (t + 1 < total) iter(t + 1, fa1, fb1, fa0, fb0);
-    }
-  } else {
-    for (int t = 0; t < total; ++t) {
-      if (issues) {  // this wave's pieces of slice t landed (S-2 younger slices may fly)
-        if (t + S - 2 < total) gl_wait_vm<PPW * (S - 2)>();
-        else gl_wait_vm<0>();
-      }
-      __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t-1's stage is free
-      __builtin_amdgcn_sched_barrier(0);
-      if (issues && t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
-      if (!computes) continue;
-      FragA fa;
-      FragB fb;
-      read_frags(t, fa, fb);
-      mfmas(fa, fb);
-    }
-  }
-
-  const float alpha = G.alpha;
-  const bool fused_k = splitk > 1 && args.counters != nullptr;
-  if (do_bias) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i) bsum[i] += __shfl_xor(bsum[i], 32, 64);  // the two k halves
-    if (h == 0) {
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int m = m0 + wm + RM * r + i;
-        if (m >= P.M) continue;
-        if (splitk > 1) {
-          float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m;
-          if (fused_k)
-            __hip_atomic_store(bp, bsum[i] * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-          else
-            *bp = bsum[i] * alpha;
-        } else {
-          P.bias_grad[m] = bsum[i] * alpha * P.bias_grad_scale;
-        }
-      }
-    }
-  }
-  // wave tile -> row pieces through a wave-private LDS scratch (the ring is free once every
-  // wave has passed its last slice); MFMA block (i, jj) row q / column c is the wave's row
-  // RM * q + i / column RN * c + jj (the permuted fragment rows)
-  __syncthreads();
-  constexpr int LPR = TN / 4;  // lanes per row
-  const int pr = lane / LPR, pc = 4 * (lane % LPR);
-  f32x4 v[Q];
-  if (computes) {
-    float* scr = reinterpret_cast<float*>(smem) + wave * (C::SCR_BYTES / 4);
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < RN; ++jj)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-          scr[(RM * row + i) * C::SCR_LD + RN * r + jj] = acc[i][jj][e] * alpha;
-        }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int q = 0; q < Q; ++q) v[q] = ld4(scr + (pr + q * (64 / LPR)) * C::SCR_LD + pc);
-  }
-  const int n = n0 + wn + pc;
-
-  if (fused_k) {
-    const long MN = (long)P.M * P.N;
-    float* slabs = args.ws + args.slab_off[pid];
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
-    if (computes && n < P.N) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int m = m0 + wm + pr + q * (64 / LPR);
-        if (m < P.M) {
-          const f32x4 x = v[q];
-          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs,
-                                                 (int)(((long)ks * MN + (long)m * P.N + n) * 4), 0, 16);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    unsigned* flag = reinterpret_cast<unsigned*>(smem + C::SMEM - 16);
-    unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
-    if (threadIdx.x == 0)
-      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
-    __syncthreads();
-    if (!*flag) return;
-    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded: no agent acquire
-    if (P.bias_grad && bx == 0 && threadIdx.x < BM && m0 + (int)threadIdx.x < P.M) {
-      const float* bp = args.ws + args.bias_off[pid] + m0 + threadIdx.x;
-      float tb = 0.f;
-      for (int s2 = 0; s2 < splitk; ++s2)
-        tb += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      P.bias_grad[m0 + threadIdx.x] = tb * P.bias_grad_scale;
-    }
-    if (!computes) return;
-    // sum in slice order 0 .. splitk-1, this split's own partial from registers; one slab's
-    // Q loads are issued together (one latency per slab, not per float4)
-    const int nc = min(n, P.N - 4);
-    long e[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) e[q] = (long)min(m0 + wm + pr + q * (64 / LPR), P.M - 1) * P.N + nc;
-    f32x4 tsum[Q];
-    for (int s2 = 0; s2 < splitk; ++s2) {
-      f32x4 x[Q];
-      if (s2 == ks) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) x[q] = v[q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) x[q] = ld4_sc1(rs, s2 * MN + e[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < Q; ++q) tsum[q] = s2 == 0 ? x[q] : tsum[q] + x[q];
-    }
-#pragma unroll
-    for (int q = 0; q < Q; ++q) v[q] = tsum[q];
-  } else if (splitk > 1) {  // two-launch form: plain slabs, splitk_reduce4_kernel combines
-    if (computes && n < P.N) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int m = m0 + wm + pr + q * (64 / LPR);
-        if (m < P.M) st4(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N + (long)m * P.N + n, v[q]);
-      }
-    }
-    return;
-  }
-  if (!computes || n >= P.N) return;
-  DropMask dm;
-  if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int m = m0 + wm + pr + q * (64 / LPR);
-    if (m < P.M) epilogue_row4(P, m, n, v[q], dm);
-  }
 }
 
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
@@ -2216,193 +1635,6 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   }
 }
 
-// ------------------------------------------------------------------------------ persistent
-// One output tile of the persistent kernel: integers only (wave-uniform).  Pointers and
-// leading dimensions are re-read from the kernel arguments (scalar loads) at each fetch,
-// which happens right after a barrier when no LDS reads are outstanding.
-struct TileInfo {
-  int pid, m0, n0, bn, ks, nsl, M, N;
-  int kb0, kb1, kb2, ke0, ke1, ke2, ns0, ns1;
-};
-
-template <int BM, int BN, int BK>
-__device__ __forceinline__ void decode_tile(const GemmArgs& a, int t, TileInfo& ti) {
-  int p = 0;
-  while (p + 1 < a.nprob && t >= a.tile_prefix[p + 1]) ++p;
-  const sca_gemm_problem& P = a.p[p];
-  const int local = t - a.tile_prefix[p];
-  const int tn = a.tiles_n[p], tm = (P.M + BM - 1) / BM;
-  ti.pid = p;
-  ti.M = P.M;
-  ti.N = P.N;
-  ti.bn = local % tn;
-  ti.ks = local / (tn * tm);
-  ti.m0 = ((local / tn) % tm) * BM;
-  ti.n0 = ti.bn * BN;
-  int kb[3], ke[3], ns[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    kb[s] = ke[s] = ns[s] = 0;
-    if (s < P.nseg) {
-      const int K = P.seg[s].K;
-      int b = 0, e = K;
-      if (a.splitk > 1) {
-        const int chunk = ((K + a.splitk - 1) / a.splitk + BK - 1) / BK * BK;
-        b = ti.ks * chunk;
-        e = min(K, b + chunk);
-      }
-      kb[s] = b;
-      ke[s] = e;
-      ns[s] = e > b ? (e - b + BK - 1) / BK : 0;
-    }
-  }
-  ti.kb0 = kb[0]; ti.kb1 = kb[1]; ti.kb2 = kb[2];
-  ti.ke0 = ke[0]; ti.ke1 = ke[1]; ti.ke2 = ke[2];
-  ti.ns0 = ns[0]; ti.ns1 = ns[1];
-  ti.nsl = ns[0] + ns[1] + ns[2];
-}
-
-// Persistent grouped GEMM: each workgroup walks its share of ALL problems' output tiles and
-// the K-slices of consecutive tiles form one continuous double-buffered pipeline: the next
-// tile's first slice is fetched while the current tile finishes, so short-K tiles
-// (K = 256..768 here) pay no per-tile pipeline fill.
-template <int LAYOUT, class C>
-__global__ __launch_bounds__(C::NT) void gemm_persistent_kernel(const GemmArgs args) {
-  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, NT = C::NT, RM = C::RM, RN = C::RN;
-  constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
-  constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
-  using OpA = Operand<A_KC, BM, BK, NT>;
-  using OpB = Operand<B_KC, BN, BK, NT>;
-  constexpr int STAGE = OpA::kLds + OpB::kLds;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
-
-  const unsigned nwg = gridDim.x;
-  const unsigned orig = blockIdx.x;
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (int)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3));
-  const int total_tiles = args.tile_prefix[args.nprob];
-  if (wgid >= total_tiles) return;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave / C::WN) * C::TM, wn = (wave % C::WN) * C::TN;
-  const int col = lane & 31;
-  const int rowh = 4 * (lane >> 5);
-
-  f32x16 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  f32x4 ra[OpA::kVec], rb[OpB::kVec];
-  float alpha_f = 1.f;
-  auto fetch = [&](const TileInfo& ti, int sl) {
-    int s = 0, kb = ti.kb0, ke = ti.ke0;
-    if (sl >= ti.ns0) {
-      sl -= ti.ns0;
-      s = 1, kb = ti.kb1, ke = ti.ke1;
-      if (sl >= ti.ns1) {
-        sl -= ti.ns1;
-        s = 2, kb = ti.kb2, ke = ti.ke2;
-      }
-    }
-    const sca_gemm_seg& S = args.p[ti.pid].seg[s];
-    const int k0 = kb + sl * BK;
-    load_tile<A_KC, BM, BK, NT>(ra, S.A, S.lda, ti.m0, ti.M, k0, ke);
-    load_tile<B_KC, BN, BK, NT>(rb, S.B, S.ldb, ti.n0, ti.N, k0, ke);
-    alpha_f = S.alpha;
-  };
-
-  float bsum = 0.f;
-  TileInfo cur, nxt;
-  int t = wgid;
-  decode_tile<BM, BN, BK>(args, t, cur);
-  int sl = 0;
-  fetch(cur, 0);
-  store_tile<A_KC, BM, BK, NT>(smem, ra, alpha_f);
-  store_tile<B_KC, BN, BK, NT>(smem + OpA::kLds, rb, 1.0f);
-  __syncthreads();
-  int buf = 0;
-  while (true) {
-    bool have_next = true;
-    int nsl_idx = sl + 1;
-    int tn = t;
-    if (nsl_idx >= cur.nsl) {
-      nsl_idx = 0;
-      tn = t + (int)nwg;
-      have_next = tn < total_tiles;
-      if (have_next) decode_tile<BM, BN, BK>(args, tn, nxt);
-    } else {
-      nxt = cur;
-    }
-    if (have_next) fetch(nxt, nsl_idx);  // in flight during the MFMAs below
-
-    const float* As = smem + buf * STAGE;
-    const float* Bs = As + OpA::kLds;
-    const sca_gemm_problem& P = args.p[cur.pid];
-    const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && cur.bn == 0;
-    if (do_bias && threadIdx.x < BM) {
-#pragma unroll 8
-      for (int k = 0; k < BK; ++k) bsum += As[k * (BM + KPAD) + threadIdx.x];  // TN: A image is [BK][BM+4]
-    }
-#pragma unroll
-    for (int g8 = 0; g8 < BK / 8; ++g8) {
-      f32x4 fa[RM], fb[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) fa[i] = read_frag<A_KC, BM, BK>(As, wm + i * 32, g8, lane);
-#pragma unroll
-      for (int j = 0; j < RN; ++j) fb[j] = read_frag<B_KC, BN, BK>(Bs, wn + j * 32, g8, lane);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int j = 0; j < RN; ++j) acc[i][j] = mfma32(fa[i][s], fb[j][s], acc[i][j]);
-    }
-    if (sl + 1 >= cur.nsl) {  // tile complete: epilogue (the next tile's loads stay in flight)
-      if (do_bias && threadIdx.x < BM && cur.m0 + (int)threadIdx.x < P.M) {
-        if (args.splitk > 1)
-          args.ws[args.bias_off[cur.pid] + (long)cur.ks * P.M + cur.m0 + threadIdx.x] = bsum;
-        else
-          P.bias_grad[cur.m0 + threadIdx.x] = bsum * P.bias_grad_scale;
-      }
-      bsum = 0.f;
-      if (args.splitk > 1) {
-        float* slab = args.ws + args.slab_off[cur.pid] + (long)cur.ks * P.M * P.N;
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int j = 0; j < RN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int m = cur.m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + rowh;
-              const int n = cur.n0 + wn + j * 32 + col;
-              if (m < P.M && n < P.N) slab[(long)m * P.N + n] = acc[i][j][r];
-            }
-      } else {
-        epilogue_block<RM, RN>(P, acc, cur.m0 + wm, cur.n0 + wn, col, rowh, args.drop_off);
-      }
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    }
-    if (!have_next) break;
-    buf ^= 1;
-    float* An = smem + buf * STAGE;
-    store_tile<A_KC, BM, BK, NT>(An, ra, alpha_f);
-    store_tile<B_KC, BN, BK, NT>(An + OpA::kLds, rb, 1.0f);
-    __syncthreads();
-    cur = nxt;
-    sl = nsl_idx;
-    t = tn;
-  }
-}
-
 // Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]); bias partials likewise.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args, int nprob) {
   const sca_gemm_problem& P = args.p[blockIdx.y];
@@ -2452,39 +1684,6 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GemmArgs args
   st4(P.C + (long)m * P.ldc + n, o);
 }
 
-int pick_grid(int tiles, int max_per_cu) {
-  int best_w = 1;
-  long best = -1;
-  for (int w = 1; w <= max_per_cu; ++w) {
-    const long span = (long)((tiles + 256 * w - 1) / (256 * w)) * w;
-    if (best < 0 || span <= best) {
-      best = span;
-      best_w = w;
-    }
-  }
-  const int g = 256 * best_w;
-  return tiles < g ? tiles : g;
-}
-
-template <int LAYOUT, class C>
-int launch_persistent(GemmArgs& a, int nprob, hipStream_t st) {
-  a.nprob = nprob;
-  a.tile_prefix[0] = 0;
-  for (int i = 0; i < nprob; ++i) {
-    const int tm = (a.p[i].M + C::BM - 1) / C::BM, tn = (a.p[i].N + C::BN - 1) / C::BN;
-    a.tiles_n[i] = tn;
-    a.tile_prefix[i + 1] = a.tile_prefix[i] + tm * tn * a.splitk;
-  }
-  const int tiles = a.tile_prefix[nprob];
-  if (tiles == 0) return SCA_OK;
-  constexpr int lds = 2 * (Operand<LAYOUT != SCA_GEMM_TN, C::BM, C::BK, C::NT>::kLds +
-                           Operand<LAYOUT == SCA_GEMM_NT, C::BN, C::BK, C::NT>::kLds) * 4;
-  int per_cu = (160 * 1024) / lds;
-  per_cu = per_cu < 4 ? (per_cu < 1 ? 1 : per_cu) : 4;
-  hipLaunchKernelGGL((gemm_persistent_kernel<LAYOUT, C>), dim3(pick_grid(tiles, per_cu)), dim3(C::NT), 0, st, a);
-  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
-}
-
 template <int LAYOUT, class C, bool VEC = true>
 int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + C::BN - 1) / C::BN, (maxM + C::BM - 1) / C::BM, nprob * a.splitk);
@@ -2492,27 +1691,24 @@ int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-// Tile configurations (index = sca_gemm_tile_override value)
+// Kernel variants (index = sca_gemm_tile_override value; every one computes the full result):
+//   1  register-staged 64x64, 4 waves (the any-shape fallback: element-wise loads)
+//   5  register-staged 64x64, single-buffered (TN fallback when the LDS-DMA kernel cannot take
+//      the shapes)
+//   7  register-staged 128x64, 8 waves (NN fallback)
+//   20 / 21 / 22  LDS-DMA 64x64 with a 3- / 2- / 4-stage ring (the heuristic's kernels)
+//   36 / 37  TN only: the k-split outer-product weight-gradient kernel, 3- / 4-stage ring
 using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
-using T2 = Cfg<128, 64, 2, 2, 32, 2>;   // 4 waves, 64x32
-using T3 = Cfg<64, 128, 2, 2, 32, 2>;   // 4 waves, 32x64
-using T4 = Cfg<128, 128, 2, 2, 32, 2>;  // 4 waves, 64x64
 using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
-using T6 = Cfg<128, 128, 2, 4, 32, 2>;  // 8 waves, 64x32
 using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
-using T8 = Cfg<64, 64, 2, 2, 64, 2>;    // BK 64
-using T9 = Cfg<64, 64, 2, 2, 16, 2>;    // BK 16
-constexpr int kNumTiles = 9;
+constexpr int kTnFirst = 36, kTnLast = 37;
 
-// persistent kernels need every tile to own >= 1 K-slice (no empty split-K chunks)
-bool persistent_ok(const GemmArgs& a, int nprob) {
-  for (int i = 0; i < nprob; ++i)
-    for (int s = 0; s < a.p[i].nseg; ++s) {
-      const int K = a.p[i].seg[s].K;
-      const int chunk = ((K + a.splitk - 1) / a.splitk + 31) / 32 * 32;
-      if (K < 1 || (a.splitk > 1 && (long)(a.splitk - 1) * chunk >= K)) return false;
-    }
-  return true;
+bool valid_tile(int layout, int tile) {
+  switch (tile) {
+    case 0: case 1: case 5: case 7: case 20: case 21: case 22: return true;
+    case 36: case 37: return layout == SCA_GEMM_TN;
+    default: return false;
+  }
 }
 
 // the LDS-DMA kernel's shape requirements (see gemm_glds_kernel)
@@ -2533,13 +1729,6 @@ int launch_glds(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-template <int LAYOUT, int S>
-int launch_glds2(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_glds2_kernel<LAYOUT, S>), grid, dim3(512), 0, st, a);
-  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
-}
-
 // float4 operand loads need K (k-contiguous operands), lda, ldb multiples of 4 and A, B
 // 16-byte aligned; otherwise the element-wise (any-shape) form of the register-staged kernel
 bool vec_ok(const GemmArgs& a, int nprob, int layout) {
@@ -2554,27 +1743,10 @@ bool vec_ok(const GemmArgs& a, int nprob, int layout) {
   return true;
 }
 
-// large-tile weight-gradient kernels (gemm_tn_kernel), index = tile - 30
-using TN0 = TnCfg<64, 64, 2, 2, 4>;             // 4 waves, 32x32 each, 4-stage ring
-using TN1 = TnCfg<64, 64, 2, 2, 4, 4>;          // + 4 loader waves
-using TN2 = TnCfg<64, 64, 2, 2, 4, 0, true>;    // 4 waves, fragments one slice ahead
-using TN3 = TnCfg<64, 64, 2, 2, 4, 4, true>;    // + 4 loader waves, fragments one slice ahead
-using TN4 = TnCfg<128, 64, 2, 2, 4, 4, true>;   // 4 compute waves 64x32 + 4 loaders, prefetch
-using TN5 = TnCfg<64, 64, 2, 2, 3, 4, true>;    // 3 stages + 4 loaders, prefetch
-// 36 .. 39: gemm_tnk_kernel, ring stages 3 / 4, fragments read in-slice (36, 37) or one slice ahead (38, 39)
-constexpr int kTnFirst = 30, kTnLast = 43;
-
-template <int S, int SUB, bool PF = false, int NODMA = 0>
+template <int S, int SUB>
 int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_tnk_kernel<S, SUB, PF, NODMA>), grid, dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
-}
-
-template <class C>
-int launch_tn(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  dim3 grid((maxN + C::BN - 1) / C::BN, (maxM + C::BM - 1) / C::BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_tn_kernel<C>), grid, dim3(C::NT), 0, st, a);
+  hipLaunchKernelGGL((gemm_tnk_kernel<S, SUB>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -2588,50 +1760,18 @@ template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
   if (tile >= kTnFirst && tile <= kTnLast) {
-    if (LAYOUT != SCA_GEMM_TN || !tn_ok(a, nprob)) {
-      tile = 21;
-    } else {
-      switch (tile) {
-        case 30: return launch_tn<TN0>(a, nprob, maxM, maxN, st);
-        case 31: return launch_tn<TN1>(a, nprob, maxM, maxN, st);
-        case 32: return launch_tn<TN2>(a, nprob, maxM, maxN, st);
-        case 33: return launch_tn<TN3>(a, nprob, maxM, maxN, st);
-        case 34: return launch_tn<TN4>(a, nprob, maxM, maxN, st);
-        case 35: return launch_tn<TN5>(a, nprob, maxM, maxN, st);
-        case 36: return launch_tnk<3, 1>(a, nprob, maxM, maxN, st);
-        case 37: return launch_tnk<4, 1>(a, nprob, maxM, maxN, st);
-        case 38: return launch_tnk<3, 1, true>(a, nprob, maxM, maxN, st);
-        case 39: return launch_tnk<4, 1, true>(a, nprob, maxM, maxN, st);
-        case 40: return launch_tnk<3, 1, false, 1>(a, nprob, maxM, maxN, st);  // timing probes
-        case 41: return launch_tnk<3, 1, true, 1>(a, nprob, maxM, maxN, st);
-        case 42: return launch_tnk<3, 1, false, 2>(a, nprob, maxM, maxN, st);
-        default: return launch_tnk<3, 1, false, 3>(a, nprob, maxM, maxN, st);
-      }
-    }
+    if (LAYOUT == SCA_GEMM_TN && tn_ok(a, nprob))
+      return tile == 36 ? launch_tnk<3, 1>(a, nprob, maxM, maxN, st) : launch_tnk<4, 1>(a, nprob, maxM, maxN, st);
+    tile = 21;
   }
-  if (tile > 10 && tile < 20 && !persistent_ok(a, nprob)) tile = 1;
   if (tile >= 20 && !glds_ok(a, nprob)) tile = LAYOUT == SCA_GEMM_TN ? 5 : (LAYOUT == SCA_GEMM_NN ? 7 : 1);
   switch (tile) {
     case 20: return launch_glds<LAYOUT, 3>(a, nprob, maxM, maxN, st);
     case 21: return launch_glds<LAYOUT, 2>(a, nprob, maxM, maxN, st);
     case 22: return launch_glds<LAYOUT, 4>(a, nprob, maxM, maxN, st);
-    case 23: return launch_glds2<LAYOUT, 3>(a, nprob, maxM, maxN, st);
-    case 24: return launch_glds2<LAYOUT, 2>(a, nprob, maxM, maxN, st);
-    case 11: return launch_persistent<LAYOUT, T1>(a, nprob, st);
-    case 12: return launch_persistent<LAYOUT, T2>(a, nprob, st);
-    case 13: return launch_persistent<LAYOUT, T3>(a, nprob, st);
-    case 14: return launch_persistent<LAYOUT, T4>(a, nprob, st);
-    case 15: return launch_persistent<LAYOUT, T6>(a, nprob, st);
-    case 16: return launch_persistent<LAYOUT, T7>(a, nprob, st);
-    case 1: return launch<LAYOUT, T1>(a, nprob, maxM, maxN, st);
-    case 2: return launch<LAYOUT, T2>(a, nprob, maxM, maxN, st);
-    case 3: return launch<LAYOUT, T3>(a, nprob, maxM, maxN, st);
-    case 4: return launch<LAYOUT, T4>(a, nprob, maxM, maxN, st);
     case 5: return launch<LAYOUT, T5>(a, nprob, maxM, maxN, st);
-    case 6: return launch<LAYOUT, T6>(a, nprob, maxM, maxN, st);
     case 7: return launch<LAYOUT, T7>(a, nprob, maxM, maxN, st);
-    case 8: return launch<LAYOUT, T8>(a, nprob, maxM, maxN, st);
-    default: return launch<LAYOUT, T9>(a, nprob, maxM, maxN, st);
+    default: return launch<LAYOUT, T1>(a, nprob, maxM, maxN, st);
   }
 }
 
@@ -2663,10 +1803,13 @@ extern "C" int sca_gemm_clk(unsigned long long* out, int n) {
 }
 #endif
 
+extern "C" void sca_set_error(const char* msg);
+
 extern "C" int sca_gemm_tile_override(int layout, int tile) {
-  if (layout < 0 || layout > 2 || tile < 0 ||
-      (tile > kNumTiles && (tile < 11 || tile > 16) && (tile < 20 || tile > 24) && (tile < kTnFirst || tile > kTnLast)))
+  if (layout < 0 || layout > 2 || !valid_tile(layout, tile)) {
+    sca_set_error("sca_gemm_tile_override: unknown layout or kernel variant id");
     return SCA_ERR_ARG;
+  }
   g_tile_override[layout] = tile;
   return SCA_OK;
 }
@@ -2676,7 +1819,7 @@ extern "C" void sca_set_error(const char* msg);
 namespace {
 // do_main: the GEMM launch; do_reduce: the split-K slab reduction (splitk > 1 only)
 int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace, void* stream,
-              bool do_main, bool do_reduce, unsigned* counters = nullptr) {
+              bool do_main, bool do_reduce, unsigned* counters = nullptr, int variant = 0) {
   if (nprob <= 0) return SCA_OK;
   if (nprob > SCA_GEMM_MAX_PROBLEMS || layout < 0 || layout > 2 || splitk < 1) {
     sca_set_error("sca_gemm: bad nprob/layout/splitk");
@@ -2740,7 +1883,7 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   int rc;
   long tiles64 = 0;
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
-  const int tile = pick_tile(layout, tiles64, splitk);
+  const int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
   const bool tn_big = layout == SCA_GEMM_TN && tile >= kTnFirst && tile <= kTnLast && tn_ok(a, nprob);
   if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&
@@ -2796,6 +1939,15 @@ extern "C" long sca_gemm_splitk_counters(int nprob, int maxM, int maxN) {
 extern "C" int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_problem* probs, int splitk,
                                      float* workspace, unsigned* counters, void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, true, counters);
+}
+
+extern "C" int sca_gemm_variant(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
+                                unsigned* counters, int variant, void* stream) {
+  if (layout < 0 || layout > 2 || !valid_tile(layout, variant)) {
+    sca_set_error("sca_gemm_variant: unknown layout or kernel variant id");
+    return SCA_ERR_ARG;
+  }
+  return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, true, counters, variant);
 }
 
 // 32-row tiles (8 waves) whenever they give a workgroup per CU, else 16-row tiles (2

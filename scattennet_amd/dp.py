@@ -164,9 +164,6 @@ class GradBuckets:
             self._step["works"].append(dist.all_reduce(self._bucket(b), async_op=True))
 
     def _finish(self):
-        # deferred weight-gradient launches (ops.SCA_WGRAD_DEFER) report their gradients when
-        # launched: launch them now, inside this step, before it is closed
-        ops.flush_weight_grads()
         st, self._step = self._step, None
         if st is None:
             return

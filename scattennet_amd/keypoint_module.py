@@ -60,7 +60,7 @@ def coordinate_attention_grouped(blocks, xs, mask, nxt=None):
 def qkv_request(blocks):
     """ops.NextProjections for the q / k / v projections of self / causal attention blocks
     (q carries the 1/sqrt(head_dim) scale, as AttentionBlock computes it)."""
-    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "fc1" or library.compiling():
+    if not ops._CHAIN_NEXT or library.compiling():
         return None
     specs = []
     for b in blocks:
@@ -87,10 +87,9 @@ class CoordinatesMerge(nn.Module):
         return coordinates_merge_grouped([self], [y_embed], [x_embed], cross_attn_mask)[0]
 
 
-def coordinates_merge_grouped(blocks, ys, xs, mask, nxt=None, kvacc=None):
+def coordinates_merge_grouped(blocks, ys, xs, mask, nxt=None):
     h = attention_grouped([b.attn for b in blocks], "cross", ys, xs, mask, resid=True, drop_p=drop_p(blocks),
-                          ln=[b.attn_layer_norm for b in blocks], nxt=fc1_request([b.mlp for b in blocks]),
-                          kvacc=kvacc)
+                          ln=[b.attn_layer_norm for b in blocks], nxt=fc1_request([b.mlp for b in blocks]))
     return ffn_grouped([b.mlp for b in blocks], h, residual=True, ln=[b.last_layer_norm for b in blocks], nxt=nxt)
 
 
@@ -164,9 +163,6 @@ def sca_grouped(scas, xs, ys, attention_mask):
     else:
         s = _self_stack(scas, s, self_mask, L)
     c = ce
-    # the merge layers all read the final x-stream map s; their backward runs L-1 .. 0, so
-    # its gradient accumulates in their GEMM epilogues instead of L-1 autograd adds
-    kvacc = ops.KvGradAccumulator() if (ops._KV_ACC and L > 1 and not library.compiling()) else None
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
         if i == 0 and branch is not None:
@@ -175,8 +171,7 @@ def sca_grouped(scas, xs, ys, attention_mask):
             for t in s:
                 t.record_stream(main)
         nxt = qkv_request([m.causal_attn_layers[i + 1] for m in scas]) if i + 1 < L else None
-        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask, nxt=nxt,
-                                      kvacc=(kvacc, i) if kvacc is not None else None)
+        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask, nxt=nxt)
     return c, s
 
 
@@ -187,7 +182,7 @@ def _self_stack(scas, s, mask, L):
     return s
 
 
-_BRANCH_OVERLAP = __import__("os").environ.get("SCA_BRANCH_OVERLAP", "1") != "0"
+_BRANCH_OVERLAP = True
 _branch_stream = ops.branch_stream
 
 

@@ -83,7 +83,7 @@ def fc1_request(ffns):
     """ops.NextProjections for the FFNs' fc1 (bias + GELU, keeping the pre-activation),
     computed in the launch that produces their input; None when not applicable (dropout
     inside the FFN, widths other than d_model = 256 / d_ff <= 768, SCA_CHAIN_NEXT=0)."""
-    if not ops._CHAIN_NEXT or ops._CHAIN_WHICH == "qkv" or drop_p(ffns) > 0 or library.compiling():
+    if not ops._CHAIN_NEXT or drop_p(ffns) > 0 or library.compiling():
         return None
     specs = [[(f.fc1.weight, f.fc1.bias, 1.0, True)] for f in ffns]
     return ops.NextProjections(specs) if ops.NextProjections.eligible(specs) else None

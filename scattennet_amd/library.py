@@ -221,7 +221,7 @@ def attention_block_backward(dy: Tensor, xq: Tensor, xkv: Optional[Tensor], para
     cross = kind == "cross"
     ctx = _Ctx()
     ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = 1, kind, num_heads, scale, plus_one, resid
-    ctx.kvacc, ctx.attn_drop, ctx.drop_p, ctx.seeds, ctx.ln = None, None, 0.0, [None], fused
+    ctx.attn_drop, ctx.drop_p, ctx.seeds, ctx.ln = None, None, 0.0, [None], fused
     ctx.bet = (ln_bias,) if fused else ()
     ctx.lnsaved = ctx.lnprev = None
     sv = [key_valid, add_mask, xq] + _opt(xkv if cross else None) + list(params) + list(saved[:6])
@@ -678,14 +678,14 @@ def _bias_list(bs):
     return [b for b in bs]
 
 
-def attention_block_apply(G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, kvacc,
-                          attn_p, *ts):
+def attention_block_apply(G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, attn_p,
+                          *ts):
     if not compiling():
         return ops.AttentionBlock.apply(G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps,
-                                        nxt, kvacc, attn_p, *ts)
+                                        nxt, attn_p, *ts)
     if drop_p > 0 or attn_p > 0:
         return _eager(ops.AttentionBlock.apply)(G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p,
-                                                ln_eps, None, None, attn_p, *ts)
+                                                ln_eps, None, attn_p, *ts)
     cross = kind == "cross"
     ln = ln_eps is not None
     o = G * (2 if cross else 1)

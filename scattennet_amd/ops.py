@@ -65,21 +65,9 @@ class _timed:
             _PROFILER.records.append((self.key, self.flops, self.e0, self.e1))
 
 
-# rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>)
-def _gemm_names():
-    """Kernel name per layout as rocprofv3 reports it (the LDS-DMA ring depth pick_tile
-    chooses: 3 stages forward, 2 for the gradient layouts; SCA_GEMM_TILES overrides)."""
-    stages = {20: 3, 21: 2, 22: 4}
-    default = {0: 20, 1: 21, 2: 21}
-    env = [t.strip() for t in __import__("os").environ.get("SCA_GEMM_TILES", "").split(",")]
-    names = {}
-    for lay in range(3):
-        t = int(env[lay]) if lay < len(env) and env[lay] not in ("", "0") else default[lay]
-        names[lay] = f"gemm_glds_kernel<{lay}, {stages[t]}>" if t in stages else f"gemm_kernel<{lay}>"
-    return names
-
-
-_GEMM_NAMES = _gemm_names()
+# rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>:
+# the ring depth pick_tile chooses, 3 stages forward, 2 for the gradient layouts)
+_GEMM_NAMES = {0: "gemm_glds_kernel<0, 3>", 1: "gemm_glds_kernel<1, 2>", 2: "gemm_glds_kernel<2, 2>"}
 
 # --------------------------------------------------------------------------- launch helpers
 _NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0)
@@ -174,7 +162,7 @@ def dropout_grouped(xs, p):
 
 
 # split-K slabs combined inside the GEMM launch by the last-arriving split (sca_gemm_splitk_fused)
-_SPLITK_FUSED = __import__("os").environ.get("SCA_SPLITK_FUSED", "1") != "0"
+_SPLITK_FUSED = True
 _CNT = {}  # device index -> [ring, position]
 _CNT_SIZE = 1 << 16
 
@@ -202,18 +190,10 @@ _TILE_NAMES = {36: "gemm_tnk_kernel<3, 1, false, 0>", 37: "gemm_tnk_kernel<4, 1,
 
 
 def gemm(layout, probs, splitk=1, ws=None, tile=0):
-    """tile: a kernel variant for this call only (sca_gemm_tile_override ids; 0 = the heuristic)."""
+    """tile: a kernel variant for this call only (sca_gemm_variant ids; 0 = the heuristic),
+    passed per call through the C ABI (no process-global override is touched)."""
     lib = L.lib()
-    if tile:
-        L.check(lib.sca_gemm_tile_override(layout, tile), "sca_gemm_tile_override")
-        try:
-            return _gemm(lib, layout, probs, splitk, ws, _TILE_NAMES.get(tile, f"gemm tile {tile}"))
-        finally:
-            lib.sca_gemm_tile_override(layout, _TN_TILE if layout == L.GEMM_TN else 0)
-    return _gemm(lib, layout, probs, splitk, ws, _GEMM_NAMES[layout])
-
-
-def _gemm(lib, layout, probs, splitk, ws, kname):
+    kname = _TILE_NAMES.get(tile, f"gemm tile {tile}") if tile else _GEMM_NAMES[layout]
     st = L.stream_handle()
     for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
@@ -224,8 +204,13 @@ def _gemm(lib, layout, probs, splitk, ws, kname):
                                                                 max(p.N for p in chunk)),
                                    ws.device.index if ws is not None else None)
             with _timed(kname, flops):
-                L.check(lib.sca_gemm_splitk_fused(layout, len(chunk), arr, splitk, ptr(ws), ptr(cnt), st),
-                        "sca_gemm_splitk_fused")
+                L.check(lib.sca_gemm_variant(layout, len(chunk), arr, splitk, ptr(ws), ptr(cnt), tile, st),
+                        "sca_gemm_variant")
+            continue
+        if tile:
+            with _timed(kname, flops):
+                L.check(lib.sca_gemm_variant(layout, len(chunk), arr, splitk, ptr(ws), None, tile, st),
+                        "sca_gemm_variant")
             continue
         with _timed(kname, flops):
             L.check(lib.sca_gemm_partial(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm")
@@ -235,18 +220,18 @@ def _gemm(lib, layout, probs, splitk, ws, kname):
 
 
 # the fused LayerNorms' dgamma / dbeta reductions ride in the weight-gradient side section
-_LN_AFFINE_SIDE = __import__("os").environ.get("SCA_LN_AFFINE_SIDE", "1") != "0"
+_LN_AFFINE_SIDE = True
 
 # GEMM + post-LN LayerNorm in one launch (sca_gemm_ln) where the shape allows it
-_FUSE_LN = __import__("os").environ.get("SCA_FUSE_LN", "1") != "0"
+_FUSE_LN = True
 
 
 # d_model 512 (two 256-column halves, no chained passes): parity-green, but slower than the
 # plain 64x64-tile GEMMs + separate LayerNorm launches at config 5 (71.9 vs 70.6 ms/step:
 # the 32-row x 256-column tiles at one workgroup per CU run the big-M GEMMs at ~0.43 of
 # peak against the plain kernel's ~0.6, which outweighs the LayerNorm launches saved;
-# tools/r03_t13.sh / r03_t14.sh) — opt-in (SCA_FUSE_LN512=1)
-_FUSE_LN512 = __import__("os").environ.get("SCA_FUSE_LN512", "0") != "0"
+# DESIGN.md §9) — opt-in (tests switch it on)
+_FUSE_LN512 = False
 
 
 def ln_width_ok(N):
@@ -277,7 +262,7 @@ def gemm_ln(probs, lns, eps):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
-_FUSE_LNB = __import__("os").environ.get("SCA_FUSE_LNB", "1") != "0"
+_FUSE_LNB = True
 
 
 class LnSaved:
@@ -306,13 +291,13 @@ def ln_saved_of(ts):
     return out if all(o is not None for o in out) else None
 
 
-_CHAIN_DO = __import__("os").environ.get("SCA_CHAIN_DO", "1") != "0"
+_CHAIN_DO = True
 # the embedding LayerNorm (position-table mode) handed to its consumer's sca_gemm_lnb
-_EMB_LNB = __import__("os").environ.get("SCA_EMB_LNB", "1") != "0"
+_EMB_LNB = True
 # the FFN's dz chained into its consumer's sca_gemm_lnb launch: parity-green, but -1.7 % in
 # step at config 2 (three 256-column passes at one workgroup per CU lose to the stand-alone
-# NN GEMM that shares the CUs with the weight gradients; tools/ab_dz.sh) — off by default
-_CHAIN_DZ = __import__("os").environ.get("SCA_CHAIN_DZ", "0") != "0"
+# NN GEMM that shares the CUs with the weight gradients) — off (tests switch it on)
+_CHAIN_DZ = False
 
 
 def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None, aux=None):
@@ -331,8 +316,7 @@ def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None, aux=None):
     return objs
 
 
-_CHAIN_NEXT = __import__("os").environ.get("SCA_CHAIN_NEXT", "1") != "0"
-_CHAIN_WHICH = __import__("os").environ.get("SCA_CHAIN_NEXT", "1")  # "fc1" / "qkv": one kind only (A/B)
+_CHAIN_NEXT = True
 
 
 class NextProjections:
@@ -404,7 +388,7 @@ def _next_of(xs):
 # workgroup per tile, so a launch of a few tiles would do them on a few CUs
 # (tools/gemm_ln_bench.py, 1 x (2048, 256, 256) + fc1: 52.8 us chained vs 28.4 us as a
 # separate 64x64-tile GEMM); the consumer then computes its projections itself
-_CHAIN_MIN_TILES = int(__import__("os").environ.get("SCA_CHAIN_MIN_TILES", "256"))
+_CHAIN_MIN_TILES = 256
 
 
 def _chain_lns(nxt, G, M, like, gam, bet, ys, means, rstds):
@@ -567,54 +551,26 @@ def reduce_rows(pairs, S, I, N, stride_s, stride_i, accumulate=False):
                 "sca_reduce_rows")
 
 
-# weight-gradient kernel experiments: SCA_TN_TILE (sca_gemm_tile_override id for the TN
-# layout: 21 = the 64x64 LDS-DMA kernel, 30-35 = gemm_tn_kernel variants) and SCA_TN_SPLITK
-# (a fixed split-K for every weight-gradient launch; 0 = the _splitk_for rule)
-_TN_TILE = int(__import__("os").environ.get("SCA_TN_TILE", "0"))
-_TN_SPLITK = int(__import__("os").environ.get("SCA_TN_SPLITK", "0"))
-_TN_SET = False
-
-
-def _tn_setup():
-    global _TN_SET
-    if not _TN_SET:
-        _TN_SET = True
-        if _TN_TILE:
-            L.check(L.lib().sca_gemm_tile_override(L.GEMM_TN, _TN_TILE), "sca_gemm_tile_override")
+_SPLITK_MAX = 8
+_SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per CU
 
 
 def _splitk_for(M_red, n_out_tiles):
-    """Split the long reduction (rows of the batch) of weight-gradient GEMMs so that the
-    grid covers the 256 CUs about four times (measured best for the concurrent side-stream
-    weight gradients: tools/gemm_bench.py and bench.py sweeps via SCA_SPLITK_TILES).
-    Default (SCA_SPLITK_ROUNDS=1): pick the split that fills whole rounds of the LDS-DMA
-    kernel's 3 workgroups per CU (768 slots) best, each split keeping >= 256 rows (+0.8 %)."""
-    if _SPLITK_ROUNDS:
-        best, best_sk = -1.0, 1
-        for sk in range(1, _SPLITK_MAX + 1):
-            if sk > 1 and M_red // sk < 256:
-                break
-            n = n_out_tiles * sk
-            if n < 512 and sk < _SPLITK_MAX and M_red // (sk + 1) >= 256:
-                continue
-            fill = n / (-(-n // _SPLITK_SLOTS) * _SPLITK_SLOTS)
-            if fill > best + 1e-9:
-                best, best_sk = fill, sk
-        return best_sk
-    sk = 1
-    while sk < _SPLITK_MAX and n_out_tiles * sk < _SPLITK_TILES and M_red // (sk * 2) >= 256:
-        sk *= 2
-    return sk
-
-
-_SPLITK_MAX = int(__import__("os").environ.get("SCA_SPLITK_MAX", "8"))
-# many-problem weight-gradient launches on gemm_tnk_kernel (+0.2-0.6 % in step, three
-# alternations, tools/r03_t16.sh); SCA_TNK_MANY=0: every TN launch on the LDS-DMA kernel
-_TNK_MANY = __import__("os").environ.get("SCA_TNK_MANY", "1") != "0"
-_SPLITK_TILES = int(__import__("os").environ.get("SCA_SPLITK_TILES", "1024"))
-_WGRAD_MIX = __import__("os").environ.get("SCA_WGRAD_MIX", "0") != "0"
-_SPLITK_ROUNDS = __import__("os").environ.get("SCA_SPLITK_ROUNDS", "1") != "0"
-_SPLITK_SLOTS = int(__import__("os").environ.get("SCA_SPLITK_SLOTS", "768"))  # workgroup slots per round
+    """Split the long reduction (rows of the batch) of weight-gradient GEMMs: the split that
+    fills whole rounds of the LDS-DMA kernel's 3 workgroups per CU (768 slots) best, each
+    split keeping >= 256 rows (+0.8 % over powers of two up to 1024 tiles; measured with
+    tools/gemm_bench.py and in-step bench A/B)."""
+    best, best_sk = -1.0, 1
+    for sk in range(1, _SPLITK_MAX + 1):
+        if sk > 1 and M_red // sk < 256:
+            break
+        n = n_out_tiles * sk
+        if n < 512 and sk < _SPLITK_MAX and M_red // (sk + 1) >= 256:
+            continue
+        fill = n / (-(-n // _SPLITK_SLOTS) * _SPLITK_SLOTS)
+        if fill > best + 1e-9:
+            best, best_sk = fill, sk
+    return best_sk
 
 
 # ---- parameter-gradient sink -------------------------------------------------------------
@@ -678,11 +634,11 @@ def params_produced(ps):
 # these sizes).  A callback queued on the autograd engine joins the side stream into the
 # caller's stream when backward() completes, so .grad is safe to read afterwards exactly as
 # with a single stream (the same mechanism torch DDP uses).  Captured into hipGraphs as a
-# fork/join.  SCA_WGRAD_STREAM=0 disables it.
+# fork/join.
 import os as _os
 
-_WGRAD_SIDE = _os.environ.get("SCA_WGRAD_STREAM", "1") != "0"
-_BRANCH_SIDE = _os.environ.get("SCA_BRANCH_SIDE", "1") != "0"  # branch-stream weight grads on their own side stream
+_WGRAD_SIDE = True
+_BRANCH_SIDE = True  # branch-stream weight grads on their own side stream
 _side_streams = {}
 _join_pending = {}
 
@@ -795,54 +751,11 @@ def _queue_join(main, side):
     _join_pending[key] = True
 
     def _join():
-        flush_weight_grads()
         _join_pending[key] = False
         main.wait_stream(side)
         note_join(main, side)
 
     torch.autograd.Variable._execution_engine.queue_callback(_join)
-
-
-# Deferred weight-gradient launches (SCA_WGRAD_DEFER=1): the side stream forks from the main
-# stream at once (its dependency set is fixed there), but its kernels are launched only after
-# the NEXT launch on the main stream.  Under graph capture the critical-path kernel is then
-# the first child of its predecessor and the weight gradients the second, so the graph
-# executor's queue assignment (child i -> queue (parent + i) mod N) keeps the
-# critical chain on one hardware queue instead of hopping (and queueing behind a weight-
-# gradient launch) at every fork.
-_WGRAD_DEFER = _os.environ.get("SCA_WGRAD_DEFER", "0") != "0"
-_PENDING_WGRAD = []  # (main stream ptr, side stream, closure)
-_FLUSHING = False
-
-
-def flush_weight_grads(after_stream=None):
-    """Launch the deferred weight-gradient closures (all, or those whose main stream is
-    `after_stream` — called after a launch on that stream)."""
-    global _FLUSHING
-    if _FLUSHING or not _PENDING_WGRAD:
-        return
-    _FLUSHING = True
-    try:
-        keep = []
-        todo = []
-        for ent in _PENDING_WGRAD:
-            (todo if after_stream is None or ent[0] == after_stream else keep).append(ent)
-        _PENDING_WGRAD[:] = keep
-        for _, side, fn in todo:
-            with torch.cuda.stream(side):
-                fn()
-    finally:
-        _FLUSHING = False
-
-
-def _post_launch():
-    if _PENDING_WGRAD and not _FLUSHING:
-        cur = torch.cuda.current_stream().cuda_stream
-        if any(ent[0] == cur for ent in _PENDING_WGRAD):
-            flush_weight_grads(cur)
-
-
-L.POST_LAUNCH = _post_launch
 
 
 def weight_grads(items, M=None, extra=None):
@@ -888,30 +801,17 @@ def weight_grads(items, M=None, extra=None):
         it[1].record_stream(side)
     for t in (extra[1] if extra is not None else ()):
         t.record_stream(side)
-    if _WGRAD_DEFER:
-        flush_weight_grads()  # earlier deferred launches keep their order on the side streams
-        with torch.cuda.stream(side):
-            out, launch = _weight_grads(items, deferred=True)
-
-        def later():
-            launch()
-            params_produced([p for it in items for p in (it[3], it[4])])
-            if extra is not None:
-                extra[0]()
-                params_produced(extra[2])
-        _PENDING_WGRAD.append((main.cuda_stream, side, later))
-    else:
-        with torch.cuda.stream(side):
-            out = run()
+    with torch.cuda.stream(side):
+        out = run()
     _queue_join(join_into, side)
     return out
 
 
-def _weight_grads(items, deferred=False):
-    """Allocate and launch; deferred=True: allocate now, return (out, launch closure)."""
+def _weight_grads(items):
+    """Allocate the gradients and launch the grouped split-K TN GEMMs."""
     out = []
     launches = []
-    by_shape = {}  # problems of one launch (SCA_WGRAD_MIX=1: any shapes, one launch)
+    by_shape = {}  # problems of one launch: one (out, in, rows) shape
     items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
     for idx, (dY, X, alpha, W, bias, _) in enumerate(items):
         n_out, n_in = W.shape
@@ -921,16 +821,15 @@ def _weight_grads(items, deferred=False):
         else:
             db = torch.empty(n_out, device=W.device, dtype=W.dtype) if bias else None
         out.append((dW, db))
-        key = (n_out, n_in, dY.shape[0]) if not _WGRAD_MIX else dY.shape[0]
+        key = (n_out, n_in, dY.shape[0])
         by_shape.setdefault(key, []).append(idx)
     for idxs in by_shape.values():
         for c in range(0, len(idxs), L.GEMM_MAX_PROBLEMS):
             sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
             tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
-            _tn_setup()
-            sk = _TN_SPLITK if _TN_SPLITK > 0 else _splitk_for(items[sub[0]][0].shape[0], tiles)
+            sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
             tile = 0
-            if _TNK_MANY and not _TN_TILE and len(sub) >= 8 and tiles >= 256:
+            if len(sub) >= 8 and tiles >= 256:
                 # many-problem launches (an attention block's q/k/v/o of every stream): the
                 # k-split outer-product kernel at split-K 2 (tools/tn_bench.py: 16 x (256 x 256,
                 # K = 2048) 0.59-0.61 of peak vs 0.57 for the 64x64 LDS-DMA kernel at split 3)
@@ -945,8 +844,6 @@ def _weight_grads(items, deferred=False):
                 wsz += sk * (n_out * n_in + n_out)
             ws = torch.empty(wsz, device=items[0][0].device, dtype=torch.float32) if sk > 1 else None
             launches.append((probs, sk, ws, tile))
-    if deferred:
-        return out, lambda: [gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl) for p, k, w, tl in launches]
     for p, k, w, tl in launches:
         gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl)
     return out
@@ -1080,25 +977,6 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
     return dq, dk, dv
 
 
-class KvGradAccumulator:
-    """One key/value input shared by a chain of cross-attention blocks whose backward passes
-    run strictly in reverse chain order (keypoint_module.sca_grouped: every merge layer reads
-    the final x-stream map, and merge i+1 consumes merge i's output).  Instead of returning
-    one gradient each for autograd to add up (3 elementwise adds per stream), the blocks'
-    key/value input-gradient GEMMs accumulate into one buffer (the first to run writes it, the
-    others add to it in their GEMM epilogue, SCA_EPI_ACCUM); the LAST block of the chain
-    (index 0, the last backward to run) returns the buffer and the others return None."""
-
-    def __init__(self):
-        self.buf = None
-
-
-# parity-green, but -1.6 % in step at config 2 (tools/ab_kvacc.sh: 1558 vs 1584 clips/s over
-# three alternations) — the autograd adds it removes run on the branch stream beside the
-# main stream's work, off the critical path; off by default (SCA_KV_ACC=1)
-_KV_ACC = __import__("os").environ.get("SCA_KV_ACC", "0") != "0"
-
-
 class AttentionBlock(Function):
     """One attention operator end to end, G streams per launch:
 
@@ -1112,8 +990,8 @@ class AttentionBlock(Function):
     into grouped split-K TN GEMMs."""
 
     @staticmethod
-    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, kvacc,
-                attn_p, *ts):
+    def forward(ctx, G, kind, H, scale, plus_one, key_valid, add_mask, has_resid, drop_p, ln_eps, nxt, attn_p,
+                *ts):
         cross = kind == "cross"
         ln = ln_eps is not None  # post-LN LayerNorm fused into the out-projection (sca_gemm_ln)
         if ln:
@@ -1173,7 +1051,6 @@ class AttentionBlock(Function):
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
-        ctx.kvacc = kvacc if cross else None  # (KvGradAccumulator, index in the chain)
         ctx.attn_drop = attn_drop
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
@@ -1227,20 +1104,15 @@ class AttentionBlock(Function):
         # input gradients (residual gradient fused as the epilogue's resid term); with `lnprev`
         # the query input's LayerNorm backward rides in the same launch (sca_gemm_lnb)
         dxq, dxkv, probs, kvprobs = [], [], [], []
-        acc = ctx.kvacc[0] if ctx.kvacc is not None else None
-        accum = acc is not None and acc.buf is not None  # an earlier (later-layer) block wrote it
-        if acc is not None and acc.buf is None:
-            acc.buf = [torch.empty_like(t) for t in xkv]
         for g in range(G):
             Wq, _, Wk, _, Wv, _ = W[6 * g:6 * g + 6]
             dqf, dkf, dvf = _flat(dq[g]), _flat(dk[g]), _flat(dv[g])
             r = _flat(dys[g]) if ctx.has_resid else None
             gx = torch.empty_like(xq[g])
             if cross:
-                gkv = acc.buf[g] if acc is not None else torch.empty_like(xkv[g])
+                gkv = torch.empty_like(xkv[g])
                 probs.append(_prob([_seg(dqf, Wq, d, d, d)], gx, B * T, d, d, resid=r, ldr=d))
-                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d,
-                                     epi=L.EPI_ACCUM if accum else 0))
+                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
                 dxkv.append(gkv)
             else:
                 probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
@@ -1267,12 +1139,7 @@ class AttentionBlock(Function):
                 dW += list(wg[4 * g + j])
             dWo.append(wg[4 * g + 3][0])
             dbo.append(wg[4 * g + 3][1])
-        if acc is not None:  # the chain's last backward hands the accumulated gradient over
-            if ctx.kvacc[1] == 0:
-                acc.buf = None
-            else:
-                dxkv = [None] * G
-        return (None,) * 13 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
+        return (None,) * 12 + tuple(dxq) + (tuple(dxkv) if cross else ()) + tuple(dW) + tuple(dWo) + \
             tuple(dbo) + dgam + dbet
 
 

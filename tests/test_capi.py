@@ -108,3 +108,20 @@ def test_state_dict_keys_match_reference():
     m = S.KeypointModule(list(range(3, 24)), fx["meta"]["T"], fx["meta"]["cfg"])
     assert set(m.state_dict().keys()) == set(fx["param"].keys())
     m.load_state_dict(fx["param"])  # strict
+
+
+def test_gemm_variant_ids_are_validated():
+    """Only kernel variants that compute the full result can be selected through the C ABI
+    (sca_gemm_tile_override / sca_gemm_variant): any other id is SCA_ERR_ARG and changes
+    nothing.  Pure argument checks — no GPU call is made."""
+    from scattennet_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    ERR, OK = 1, 0
+    for layout, bad in [(2, 40), (2, 43), (2, 30), (2, 23), (0, 36), (1, 37), (0, 11), (0, 2), (0, 99), (3, 0), (-1, 0)]:
+        assert lib.sca_gemm_tile_override(layout, bad) == ERR, (layout, bad)
+        assert lib.sca_gemm_variant(layout, 0, None, 1, None, None, bad, None) == ERR, (layout, bad)
+    for layout, good in [(0, 20), (1, 21), (2, 36), (2, 37), (2, 5), (1, 7), (0, 1), (2, 0)]:
+        assert lib.sca_gemm_tile_override(layout, good) == OK, (layout, good)
+        assert lib.sca_gemm_variant(layout, 0, None, 1, None, None, good, None) == OK, (layout, good)
+    for layout in range(3):
+        assert lib.sca_gemm_tile_override(layout, 0) == OK

@@ -13,8 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 9: "64bk16", 20: "G64s3", 21: "G64s2", 22: "G64s4", 23: "G2x64s3",
-         24: "G2x64s2", 11: "P64x64", 12: "P128x64", 14: "P128sq", 15: "P128sq8w", 16: "P128x64w8"}
+TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4"}
 
 
 def make_case(name, layout, shapes, splitk=1, segs=1):

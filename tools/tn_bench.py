@@ -51,7 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--tiles", default="21,30,31,32,33,34,35")
+    ap.add_argument("--tiles", default="21,36,37")
     ap.add_argument("--splits", default="1,2,3,4,6")
     args = ap.parse_args()
     tiles = [int(t) for t in args.tiles.split(",")]
