@@ -78,6 +78,11 @@ typedef struct {
   int K;       /* reduction length of this segment (any: K, lda, ldb not multiples of 4 or
                   operands not 16-byte aligned take the element-wise load form) */
   float alpha; /* scales A on load: alpha=0.5 reproduces v_proj(kv/2) exactly */
+  /* optional: B already split into its three bf16 pieces by sca_split3 (planes of B's own
+   * layout and leading dimension ldb, `bs_plane` elements apart), read instead of B by the
+   * x6 kernels (NT / NN); NULL = B is split inside the GEMM */
+  const unsigned short* Bs;
+  long bs_plane;
 } sca_gemm_seg;
 
 typedef struct {
@@ -213,6 +218,19 @@ typedef struct {
 
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);
 int sca_gemm_lnb_blocks(int M);
+
+/* fp32 -> the three bf16 pieces of the x6 GEMMs (include/scatten.h, sca_gemm_seg.Bs):
+ * dst[p * plane + i] = piece p of src[i], x = hi + mid + lo (round to nearest at each step;
+ * the residual is below 2^-24 |x|).  One launch over up to SCA_SPLIT_MAX_PROBLEMS arrays —
+ * every Linear weight of a step at once.                                                  */
+typedef struct {
+  const float* src;
+  unsigned short* dst;
+  long n;     /* elements */
+  long plane; /* elements between dst's planes (>= n) */
+} sca_split_problem;
+#define SCA_SPLIT_MAX_PROBLEMS 64
+int sca_split3(int nprob, const sca_split_problem* probs, void* stream);
 
 /* Tuning knob: force the kernel variant of one layout for every later sca_gemm* call
  * (0 = built-in heuristic; 1 / 5 / 7 register-staged 64x64 / single-buffered 64x64 /

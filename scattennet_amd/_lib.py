@@ -27,11 +27,13 @@ POOL_MAX_PROBLEMS = 8
 SOFTMAX_MAX_PROBLEMS = 8
 GELU_MAX_PROBLEMS = 8
 DROPOUT_MAX_PROBLEMS = 12
+SPLIT_MAX_PROBLEMS = 64
 ACT_NONE, ACT_RELU = 0, 1
 
 
 class GemmSeg(ctypes.Structure):
-    _fields_ = [("A", c_void_p), ("B", c_void_p), ("lda", c_int), ("ldb", c_int), ("K", c_int), ("alpha", c_float)]
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("lda", c_int), ("ldb", c_int), ("K", c_int), ("alpha", c_float),
+                ("Bs", c_void_p), ("bs_plane", c_long)]
 
 
 class GemmProblem(ctypes.Structure):
@@ -99,6 +101,10 @@ class DropoutProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("seed", c_u64)]
 
 
+class SplitProblem(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("n", c_long), ("plane", c_long)]
+
+
 class ReduceProblem(ctypes.Structure):
     _fields_ = [("inp", c_void_p), ("out", c_void_p), ("scale", c_float)]
 
@@ -123,6 +129,7 @@ EXPORTS = {
     "sca_gemm_splitk_fused": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_variant": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
+    "sca_split3": ([c_int, c_void_p, c_void_p], c_int),
     "sca_gemm_ln_rows": ([c_int, c_int, c_int], c_int),
     "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_lnb_blocks": ([c_int], c_int),

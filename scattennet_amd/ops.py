@@ -70,11 +70,14 @@ class _timed:
 _GEMM_NAMES = {0: "gemm_glds_kernel<0, 3>", 1: "gemm_glds_kernel<1, 2>", 2: "gemm_glds_kernel<2, 2>"}
 
 # --------------------------------------------------------------------------- launch helpers
-_NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0)
+_NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0, None, 0)
 
 
-def _seg(A, B, lda, ldb, K, alpha=1.0):
-    return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha)
+def _seg(A, B, lda, ldb, K, alpha=1.0, Bs=None):
+    """Bs: B's three bf16 pieces (planes_of(B) / split3), read by the x6 kernels instead of B."""
+    if Bs is None:
+        return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha, None, 0)
+    return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha, Bs.ptr_for(B), Bs.plane)
 
 
 def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=0, aux=None, ldx=0,
@@ -87,6 +90,41 @@ def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=
     return L.GemmProblem((L.GemmSeg * 3)(*s), len(segs), M, N, C.data_ptr(), ldc, epi, ptr(bias), post_scale,
                          ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo, ptr(bias_grad), bias_grad_scale,
                          seed, p)
+
+
+# --------------------------------------------------------------------------- x6 operand planes
+class Planes:
+    """The three bf16 pieces of an fp32 tensor (sca_split3; include/scatten.h): `t` holds
+    [3][plane] 16-bit values, piece p of element i at t[p * plane + i].  A GEMM segment whose B
+    operand is (a row block of) the source tensor reads them instead of splitting B itself."""
+    __slots__ = ("t", "base_ptr", "plane", "numel")
+
+    def __init__(self, src):
+        self.numel = src.numel()
+        self.plane = -(-self.numel // 8) * 8
+        self.t = torch.empty(3 * self.plane, dtype=torch.int16, device=src.device)
+        self.base_ptr = src.data_ptr()
+
+    def ptr_for(self, B):
+        """Address of B's first element in plane 0 (B a view into the split tensor)."""
+        off = B.data_ptr() - self.base_ptr
+        if off < 0 or off >= 4 * self.numel:
+            raise ValueError("Planes.ptr_for: tensor is not a view of the split source")
+        return self.t.data_ptr() + off // 2
+
+
+def split3(srcs):
+    """Planes of each contiguous fp32 tensor in `srcs`, one sca_split3 launch per 64."""
+    out = [Planes(s) for s in srcs]
+    lib = L.lib()
+    st = L.stream_handle()
+    for c in range(0, len(srcs), L.SPLIT_MAX_PROBLEMS):
+        chunk = list(zip(srcs[c:c + L.SPLIT_MAX_PROBLEMS], out[c:c + L.SPLIT_MAX_PROBLEMS]))
+        arr = (L.SplitProblem * len(chunk))(*[L.SplitProblem(s.data_ptr(), p.t.data_ptr(), p.numel, p.plane)
+                                              for s, p in chunk])
+        with _timed("split3_kernel", 0.0):
+            L.check(lib.sca_split3(len(chunk), arr, st), "sca_split3")
+    return out
 
 
 # --------------------------------------------------------------------------- dropout

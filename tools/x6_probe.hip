@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <type_traits>
 #include <vector>
 
 #include "../include/scatten.h"
@@ -34,12 +35,13 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 struct Prob {
   const float* A;
   const float* B;
+  const unsigned short* Bp;  // pre-split B planes [3][...][K] (NT only), plane stride bplane
+  long bplane;
   float* C;
   int M, N, K, lda, ldb, ldc;
 };
 struct Args {
   Prob p[16];
-  int tiles_n[16];
   int splitk;
 };
 
@@ -135,6 +137,34 @@ struct Stage {
   }
 };
 
+// pre-split k-contiguous operand: three bf16 planes [3][rows][ld] (no VALU in the stage)
+template <int ROWS, int BK>
+struct StageP {
+  static constexpr int NV = ROWS * BK / 4 / 256;
+  uint2 v[3 * NV];
+  __device__ __forceinline__ void load(const unsigned short* base, long plane, int ld, int r0, int k0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      const int row = e / (BK / 4), kq = e % (BK / 4);
+      const unsigned short* p = base + (long)(r0 + row) * ld + k0 + 4 * kq;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[3 * i + q] = *(const uint2*)(p + q * plane);
+    }
+  }
+  __device__ __forceinline__ void store(char* img) {
+    using I = Img<ROWS, BK>;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = threadIdx.x + i * 256;
+      const int row = e / (BK / 4), kq = e % (BK / 4);
+      char* p = img + row * I::PITCH + kq * 8;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) *(uint2*)(p + q * I::PIECE) = v[3 * i + q];
+    }
+  }
+};
+
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *(const bf16x8*)p; }
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -142,9 +172,10 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 }
 
 // LAYOUT 0 NT (A[M,K], B[N,K]), 1 NN (A[M,K], B[K,N]), 2 TN (A[K,M], B[K,N])
-template <int LAYOUT, int BM, int BN, int BK>
+template <int LAYOUT, int BM, int BN, int BK, bool PREB = false>
 __global__ __launch_bounds__(256) void x6_kernel(const Args args) {
   constexpr bool AKC = LAYOUT != 2, BKC = LAYOUT == 0;
+  static_assert(!PREB || LAYOUT == 0, "pre-split B: NT only");
   using IA = Img<BM, BK>;
   using IB = Img<BN, BK>;
   constexpr int STAGEB = IA::BYTES + IB::BYTES;
@@ -152,7 +183,7 @@ __global__ __launch_bounds__(256) void x6_kernel(const Args args) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGEB];
 
   const Prob& P = args.p[blockIdx.y];
-  const int tn = args.tiles_n[blockIdx.y];
+  const int tn = (P.N + BN - 1) / BN;
   const int tiles_mn = ((P.M + BM - 1) / BM) * tn;
   const int kz = blockIdx.x / tiles_mn;
   const int t = blockIdx.x % tiles_mn;
@@ -167,7 +198,12 @@ __global__ __launch_bounds__(256) void x6_kernel(const Args args) {
   const int r = lane & 31, h = lane >> 5;
 
   Stage<AKC, BM, BK> sa;
-  Stage<BKC, BN, BK> sb;
+  using SB = typename std::conditional<PREB, StageP<BN, BK>, Stage<BKC, BN, BK>>::type;
+  SB sb;
+  auto load_b = [&](int k0) {
+    if constexpr (PREB) sb.load(P.Bp, P.bplane, P.ldb, n0, k0);
+    else sb.load(P.B, P.ldb, n0, k0);
+  };
   f32x16 acc[RM][RN];
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -175,7 +211,7 @@ __global__ __launch_bounds__(256) void x6_kernel(const Args args) {
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x16){};
 
   sa.load(P.A, P.lda, m0, kbeg);
-  sb.load(P.B, P.ldb, n0, kbeg);
+  load_b(kbeg);
   sa.store(smem);
   sb.store(smem + IA::BYTES);
   __syncthreads();
@@ -184,7 +220,7 @@ __global__ __launch_bounds__(256) void x6_kernel(const Args args) {
     const char* st = smem + (kt & 1) * STAGEB;
     if (kt + 1 < nk) {
       sa.load(P.A, P.lda, m0, kbeg + (kt + 1) * BK);
-      sb.load(P.B, P.ldb, n0, kbeg + (kt + 1) * BK);
+      load_b(kbeg + (kt + 1) * BK);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
@@ -246,16 +282,16 @@ static void fill(std::vector<float>& v, unsigned seed) {
   }
 }
 
-template <int LAYOUT, int BM, int BN, int BK>
+template <int LAYOUT, int BM, int BN, int BK, bool PREB = false>
 static float run_x6(const Args& a, int nprob, int maxM, int maxN, hipStream_t st, int iters) {
   const int tiles = ((maxM + BM - 1) / BM) * ((maxN + BN - 1) / BN) * a.splitk;
   dim3 grid(tiles, nprob);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((x6_kernel<LAYOUT, BM, BN, BK>), grid, dim3(256), 0, st, a);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((x6_kernel<LAYOUT, BM, BN, BK, PREB>), grid, dim3(256), 0, st, a);
   CK(hipEventRecord(e0, st));
-  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((x6_kernel<LAYOUT, BM, BN, BK>), grid, dim3(256), 0, st, a);
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((x6_kernel<LAYOUT, BM, BN, BK, PREB>), grid, dim3(256), 0, st, a);
   CK(hipEventRecord(e1, st));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -291,6 +327,32 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&ws, szC * cs.nprob * 4 + 1024 * 1024 * 64));
     CK(hipMemcpy(dA, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dB, hB.data(), hB.size() * 4, hipMemcpyHostToDevice));
+    // host RNE split of B into three bf16 planes (NT pre-split variants)
+    std::vector<unsigned short> hBp(3 * hB.size());
+    auto rne = [](float f) -> unsigned short {
+      unsigned u;
+      memcpy(&u, &f, 4);
+      return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    };
+    auto bf = [](unsigned short h) -> float {
+      unsigned u = (unsigned)h << 16;
+      float f;
+      memcpy(&f, &u, 4);
+      return f;
+    };
+    for (size_t i = 0; i < hB.size(); ++i) {
+      float x = hB[i];
+      unsigned short h = rne(x);
+      x -= bf(h);
+      unsigned short m = rne(x);
+      x -= bf(m);
+      hBp[i] = h;
+      hBp[hB.size() + i] = m;
+      hBp[2 * hB.size() + i] = rne(x);
+    }
+    unsigned short* dBp;
+    CK(hipMalloc(&dBp, hBp.size() * 2));
+    CK(hipMemcpy(dBp, hBp.data(), hBp.size() * 2, hipMemcpyHostToDevice));
     Args a;
     memset(&a, 0, sizeof a);
     a.splitk = cs.splitk;
@@ -299,6 +361,8 @@ int main(int argc, char** argv) {
       Prob& p = a.p[i];
       p.A = dA + szA * i;
       p.B = dB + szB * i;
+      p.Bp = dBp + szB * i;
+      p.bplane = (long)hB.size();
       p.C = dC + szC * i;
       p.M = cs.M;
       p.N = cs.N;
@@ -334,8 +398,10 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     const float t_lib = ms * 1000.f / iters;
     printf("%-32s lib fp32 %7.1f us %6.1f TF\n", cs.name, t_lib, gf / t_lib * 1e-3 * 1e3);
-    float tt[6] = {0};
-    const char* tn[6] = {"128x128x16", "128x64x32", "64x128x32", "64x64x32", "128x128x32", "128x64x16"};
+    float tt[8] = {0};
+    const char* tn[8] = {"128x128x16", "128x64x32", "64x128x32", "64x64x32", "128x128x32", "128x64x16",
+                         "P128x128x16", "P128x64x32"};
+    int nv = 6;
     switch (L) {
       case 0:
         tt[0] = run_x6<0, 128, 128, 16>(a, cs.nprob, cs.M, cs.N, st, iters);
@@ -344,6 +410,9 @@ int main(int argc, char** argv) {
         tt[3] = run_x6<0, 64, 64, 32>(a, cs.nprob, cs.M, cs.N, st, iters);
         tt[4] = run_x6<0, 128, 128, 32>(a, cs.nprob, cs.M, cs.N, st, iters);
         tt[5] = run_x6<0, 128, 64, 16>(a, cs.nprob, cs.M, cs.N, st, iters);
+        tt[6] = run_x6<0, 128, 128, 16, true>(a, cs.nprob, cs.M, cs.N, st, iters);
+        tt[7] = run_x6<0, 128, 64, 32, true>(a, cs.nprob, cs.M, cs.N, st, iters);
+        nv = 8;
         break;
       case 1:
         tt[0] = run_x6<1, 128, 128, 16>(a, cs.nprob, cs.M, cs.N, st, iters);
@@ -362,7 +431,7 @@ int main(int argc, char** argv) {
         tt[5] = run_x6<2, 128, 64, 16>(a, cs.nprob, cs.M, cs.N, st, iters);
         break;
     }
-    for (int v = 0; v < 6; ++v) printf("    x6 %-11s %7.1f us %6.1f TF(fp32-eq)\n", tn[v], tt[v], gf / tt[v] * 1e3);
+    for (int v = 0; v < nv; ++v) printf("    x6 %-11s %7.1f us %6.1f TF(fp32-eq)\n", tn[v], tt[v], gf / tt[v] * 1e3);
     CK(hipStreamSynchronize(st));
     CK(hipGetLastError());
     // accuracy (last x6 variant's output in dC, library's in dC2 / ws): problem 0, split 0
@@ -396,6 +465,7 @@ int main(int argc, char** argv) {
     CK(hipFree(dC));
     CK(hipFree(dC2));
     CK(hipFree(ws));
+    CK(hipFree(dBp));
   }
   return 0;
 }
