@@ -431,6 +431,8 @@ constexpr int GL_OP_BYTES = GL_BM * GL_BK * 4;  // 8 KiB per operand per stage
 
 __device__ __forceinline__ int gl_swz(int row) { return (row >> 1) & 7; }
 
+// (a global_load_lds builtin given a non-float source pointer silently drops the host launch
+// stubs of the kernels using it — bf16 sources go through this float* form)
 __device__ __forceinline__ void gl_dma(const float* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -1368,9 +1370,7 @@ __global__ __launch_bounds__(256) void gemm_x6d_kernel(const GemmArgs args) {
     for (int c = 0; c < A_DMA; ++c) gl_dma(pa[c] + kk * BK, base + (wave * A_DMA + c) * 1024);
 #pragma unroll
     for (int c = 0; c < B_DMA; ++c)
-      __builtin_amdgcn_global_load_lds(pb[c] + kk * stepB,
-                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (wave * B_DMA + c) * 1024),
-                                       16, 0, 0);
+      gl_dma(reinterpret_cast<const float*>(pb[c] + kk * stepB), base + A_BYTES + (wave * B_DMA + c) * 1024);
   };
 
   f32x16 acc[RM][RN];
