@@ -2353,7 +2353,7 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
           default: return launch_x6d<LAYOUT, 64, 128, 4>(a, nprob, maxM, maxN, st);
         }
     }
-    tile = 50;
+    tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;  // not eligible (e.g. no pre-split B): fp32 kernels
   }
   if (tile >= 50) {
     const int bk = (tile == 50 || tile == 55 || tile == 56) ? 16 : 32;
@@ -2384,11 +2384,14 @@ int g_tile_override[3] = {0, 0, 0};
 // Tile heuristic (measured with tools/gemm_bench.py at the workload's shapes, see
 // DESIGN.md): the 3-stage LDS-DMA 64x64 kernel wins every layout; ineligible shapes fall
 // back to 64x64 / 4 waves (NT), 128x64 / 8 waves (NN), single-buffered 64x64 (TN).
-int pick_tile(int layout, long tiles64, int splitk) {
+int pick_tile(int layout, long tiles64, int splitk, bool planes) {
   if (g_tile_override[layout]) return g_tile_override[layout];
   (void)splitk;
-  (void)tiles64;
-  // LDS-DMA kernel; launch_tile falls back per layout when a shape is not eligible.  The
+  // NT / NN with pre-split weights: the x6 LDS-DMA kernel, 128x128 tiles when they still
+  // cover the 256 CUs, else 64x128 (launch_tile falls back to the fp32 kernels when a shape
+  // is not eligible)
+  if (planes && layout != SCA_GEMM_TN) return tiles64 / 4 >= 256 ? 60 : 62;
+  // LDS-DMA fp32 kernel; launch_tile falls back per layout when a shape is not eligible.  The
   // input- and weight-gradient layouts use the 2-stage ring (32 KB: up to 5 workgroups / CU
   // beside the concurrent streams' kernels; bench.py A/B +0.9 %), the forward 3 stages.
   return layout == SCA_GEMM_NT ? 20 : 21;
@@ -2487,10 +2490,14 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   int rc;
   long tiles64 = 0;
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
-  const int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
+  bool planes = layout != SCA_GEMM_TN;
+  for (int i = 0; i < nprob; ++i)
+    for (int sg = 0; sg < probs[i].nseg; ++sg) planes = planes && probs[i].seg[sg].Bs != nullptr;
+  const int tile = variant ? variant : pick_tile(layout, tiles64, splitk, planes);
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
   const bool tn_big = layout == SCA_GEMM_TN && tile >= kTnFirst && tile <= kTnLast && tn_ok(a, nprob);
-  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&
+  const bool x6 = tile >= 50 && x6_ok(a, nprob, (tile == 50 || tile == 55 || tile == 56 || tile >= 60) ? 16 : 32);
+  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big || x6) && glds_ok(a, nprob) &&
       vec_ok(a, nprob, layout)) {
     a.counters = counters;
     do_reduce = false;

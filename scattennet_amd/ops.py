@@ -113,6 +113,72 @@ class Planes:
         return self.t.data_ptr() + off // 2
 
 
+# fp32 products on the bf16 matrix cores (csrc/x6.h): the Linear weights are split once per
+# forward pass and the NT / NN GEMMs that read them run the x6 LDS-DMA kernel.  False: every
+# GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32) — the same results to fp32 rounding.
+X6 = True
+_PLANES = None  # id(weight) -> Planes inside a weight_planes scope
+
+
+class weight_planes:
+    """One forward pass's weight planes: the 2-D fp32 weights in `weights` are split in one
+    sca_split3 launch (per 64) on entry, and every GEMM reading one of them uses its planes —
+    in the forward, and in the backward through the references the Functions keep.  Under
+    graph capture the split launch is part of the step, so replays see the current weights.
+    A nested scope reuses the outer one."""
+
+    def __init__(self, weights):
+        self.weights = weights
+
+    def __enter__(self):
+        global _PLANES
+        self.prev = _PLANES
+        if X6 and _PLANES is None and not _LIBRARY_MODE:
+            seen, ws = set(), []
+            for w in self.weights:
+                if (w is not None and w.dim() == 2 and w.is_cuda and w.dtype == torch.float32 and
+                        w.is_contiguous() and id(w) not in seen):
+                    seen.add(id(w))
+                    ws.append(w)
+            _PLANES = dict(zip(map(id, ws), split3(ws))) if ws else {}
+        return self
+
+    def __exit__(self, *exc):
+        global _PLANES
+        _PLANES = self.prev
+
+
+def linear_weights(mods):
+    """The nn.Linear weights under the modules `mods` (what the x6 GEMMs read as B)."""
+    return [m.weight for mod in mods for m in mod.modules() if isinstance(m, torch.nn.Linear)]
+
+
+def wplanes(Ws):
+    """id(W) -> Planes for the weights Ws (x6 on): from the enclosing weight_planes scope,
+    the missing ones split now in one launch.  Empty when x6 is off."""
+    if not X6 or _LIBRARY_MODE:
+        return {}
+    out, miss = {}, []
+    for w in Ws:
+        p = _PLANES.get(id(w)) if _PLANES is not None else None
+        if p is not None and p.base_ptr == w.data_ptr():
+            out[id(w)] = p
+        elif w.is_contiguous() and id(w) not in out:
+            miss.append(w)
+    if miss:
+        uniq = list({id(w): w for w in miss}.values())
+        for w, p in zip(uniq, split3(uniq)):
+            out[id(w)] = p
+            if _PLANES is not None:
+                _PLANES[id(w)] = p
+    return out
+
+
+def _wseg(A, W, lda, ldb, K, pl, alpha=1.0):
+    """A GEMM segment whose B operand is the weight W (its planes from `pl` when present)."""
+    return _seg(A, W, lda, ldb, K, alpha, Bs=pl.get(id(W)) if pl else None)
+
+
 def split3(srcs):
     """Planes of each contiguous fp32 tensor in `srcs`, one sca_split3 launch per 64."""
     out = [Planes(s) for s in srcs]
@@ -1043,6 +1109,7 @@ class AttentionBlock(Function):
         W = ts[o_:o_ + 6 * G]
         Wo, bo = ts[o_ + 6 * G:o_ + 7 * G], ts[o_ + 7 * G:o_ + 8 * G]
         L.require_device(*xq, *xkv)
+        pl = wplanes([W[6 * g + j] for g in range(G) for j in (0, 2, 4)] + list(Wo))
         B, T, d = xq[0].shape
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
@@ -1065,9 +1132,9 @@ class AttentionBlock(Function):
                 q.append(xq[g].new_empty(B, T, d))
                 k.append(xq[g].new_empty(B, Tk, d))
                 v.append(xq[g].new_empty(B, Tk, d))
-                probs.append(_prob([_seg(xf, Wq, d, d, d)], q[g], B * T, d, d, bias=bq, post_scale=scale))
-                probs.append(_prob([_seg(kf, Wk, d, d, d)], k[g], B * Tk, d, d, bias=bk))
-                probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
+                probs.append(_prob([_wseg(xf, Wq, d, d, d, pl)], q[g], B * T, d, d, bias=bq, post_scale=scale))
+                probs.append(_prob([_wseg(kf, Wk, d, d, d, pl)], k[g], B * Tk, d, d, bias=bk))
+                probs.append(_prob([_wseg(kf, Wv, d, d, d, pl, av)], v[g], B * Tk, d, d, bias=bv))
             gemm(L.GEMM_NT, probs)
         # attention-probability dropout (attention.py:67-69): its seeds precede the block's own
         attn_drop = (attn_p, dropout_seeds(G)) if attn_p > 0 else None
@@ -1079,7 +1146,7 @@ class AttentionBlock(Function):
             vs, ys, means, rstds = _ln_fwd_outputs(xq)
         else:
             ys = vs = [torch.empty_like(x) for x in xq]
-        probs = [_prob([_seg(_flat(o[g]), Wo[g], d, d, d)], vs[g], B * T, d, d, bias=bo[g],
+        probs = [_prob([_wseg(_flat(o[g]), Wo[g], d, d, d, pl)], vs[g], B * T, d, d, bias=bo[g],
                        resid=_flat(xq[g]) if has_resid else None, ldr=d,
                        drop=(seeds[g], drop_p) if drop_p > 0 else None) for g in range(G)]
         if ln:
@@ -1090,6 +1157,7 @@ class AttentionBlock(Function):
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
         ctx.attn_drop = attn_drop
+        ctx.pl = pl
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
         ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, Wo if drop_p == 0 else None) if ln else None
@@ -1117,6 +1185,7 @@ class AttentionBlock(Function):
         B, T, d = xq[0].shape
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
+        pl = getattr(ctx, "pl", None)
         dgam = dbet = ()
         ln_finish = None
         do = None
@@ -1134,7 +1203,7 @@ class AttentionBlock(Function):
         # out-projection: dO = dY' Wo (unless the consumer's sca_gemm_lnb already chained it)
         if do is None:
             do = [torch.empty_like(t) for t in o]
-            gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
+            gemm(L.GEMM_NN, [_prob([_wseg(_flat(dyo[g]), Wo[g], d, d, d, pl)], do[g], B * T, d, d) for g in range(G)])
         # dq comes back pre-multiplied by the q scale and dv by alpha_v, so that every GEMM below
         # runs with unit segment scales: dX = dq' Wq + dk Wk + dv' Wv, dWq = dq'^T x, ...
         dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do,
@@ -1149,11 +1218,12 @@ class AttentionBlock(Function):
             gx = torch.empty_like(xq[g])
             if cross:
                 gkv = torch.empty_like(xkv[g])
-                probs.append(_prob([_seg(dqf, Wq, d, d, d)], gx, B * T, d, d, resid=r, ldr=d))
-                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
+                probs.append(_prob([_wseg(dqf, Wq, d, d, d, pl)], gx, B * T, d, d, resid=r, ldr=d))
+                kvprobs.append(_prob([_wseg(dkf, Wk, d, d, d, pl), _wseg(dvf, Wv, d, d, d, pl)], gkv, B * Tk, d, d))
                 dxkv.append(gkv)
             else:
-                probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
+                probs.append(_prob([_wseg(dqf, Wq, d, d, d, pl), _wseg(dkf, Wk, d, d, d, pl),
+                                    _wseg(dvf, Wv, d, d, d, pl)],
                                    gx, B * T, d, d, resid=r, ldr=d))
             dxq.append(gx)
         if ctx.lnprev is not None:
@@ -1192,17 +1262,18 @@ class LinearResidual(Function):
         W, b = ts[G:2 * G], ts[2 * G:3 * G]
         r = _contig(ts[3 * G:4 * G]) if has_r else [None] * G
         L.require_device(*x)
+        pl = wplanes(W)
         probs, ys = [], []
         for g in range(G):
             n_out, n_in = W[g].shape
             lead = x[g].shape[:-1]
             M = x[g].numel() // n_in
             y = x[g].new_empty(*lead, n_out)
-            probs.append(_prob([_seg(_flat(x[g]), W[g], n_in, n_in, n_in)], y, M, n_out, n_out, bias=b[g],
+            probs.append(_prob([_wseg(_flat(x[g]), W[g], n_in, n_in, n_in, pl)], y, M, n_out, n_out, bias=b[g],
                                resid=r[g], ldr=n_out))
             ys.append(y)
         gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.has_r, ctx.b = G, has_r, tuple(b)  # biases: parameters (leaves) or None
+        ctx.G, ctx.has_r, ctx.b, ctx.pl = G, has_r, tuple(b), pl  # biases: parameters (leaves) or None
         ctx.save_for_backward(*x, *W)
         return tuple(ys)
 
@@ -1217,7 +1288,8 @@ class LinearResidual(Function):
             n_out, n_in = W[g].shape
             M = x[g].numel() // n_in
             dx = torch.empty_like(x[g])
-            probs.append(_prob([_seg(_flat(dys[g]), W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
+            probs.append(_prob([_wseg(_flat(dys[g]), W[g], n_out, n_in, n_out, getattr(ctx, "pl", None))], dx, M,
+                               n_in, n_in))
             dxs.append(dx)
         gemm(L.GEMM_NN, probs)
         wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
@@ -1240,6 +1312,7 @@ class FeedForwardResidual(Function):
         if ln:
             gam, bet = ts[5 * G:6 * G], ts[6 * G:7 * G]
         L.require_device(*x)
+        pl = wplanes(list(W1) + list(W2))
         B, T, d = x[0].shape
         M = B * T
         F_ = W1[0].shape[0]
@@ -1258,14 +1331,14 @@ class FeedForwardResidual(Function):
         else:
             zs = [x[0].new_empty(M, F_) for _ in range(G)]
             acts = [x[0].new_empty(M, F_) for _ in range(G)]
-            gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
+            gemm(L.GEMM_NT, [_prob([_wseg(_flat(x[g]), W1[g], d, d, d, pl)], acts[g], M, F_, F_, bias=b1[g],
                                    epi=L.EPI_GELU, aux_out=zs[g], ldo=F_,
                                    drop=(s1[g], drop_p) if drop_p > 0 else None) for g in range(G)])
         if ln:
             vs, ys, means, rstds = _ln_fwd_outputs(x)
         else:
             ys = vs = [torch.empty_like(x[g]) for g in range(G)]
-        probs = [_prob([_seg(acts[g], W2[g], F_, F_, F_)], vs[g], M, d, d, bias=b2[g],
+        probs = [_prob([_wseg(acts[g], W2[g], F_, F_, F_, pl)], vs[g], M, d, d, bias=b2[g],
                        resid=_flat(x[g]) if has_r else None, ldr=d,
                        drop=(s2[g], drop_p) if drop_p > 0 else None) for g in range(G)]
         if ln:
@@ -1275,6 +1348,7 @@ class FeedForwardResidual(Function):
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
+        ctx.pl = pl
         ctx.b1, ctx.b2, ctx.bet = tuple(b1), tuple(b2), (tuple(bet) if ln else ())  # parameters (leaves)
         # dz = (dL/dv W2) * gelu'(z) chained into the consumer's launch (no dropout in between)
         dz_chain = drop_p == 0 and _CHAIN_DZ
@@ -1289,6 +1363,7 @@ class FeedForwardResidual(Function):
         G = ctx.G
         sv = ctx.saved_tensors
         x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
+        pl = getattr(ctx, "pl", None)
         dgam = dbet = ()
         ln_finish = dzc = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
@@ -1310,12 +1385,12 @@ class FeedForwardResidual(Function):
             dz = [t.reshape(M, F_) for t in dzc]
         else:
             dz = [x[0].new_empty(M, F_) for _ in range(G)]
-            gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
+            gemm(L.GEMM_NN, [_prob([_wseg(_flat(dyo[g]), W2[g], d, F_, d, pl)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
                                    aux=zs[g], ldx=F_, drop=(ctx.s1[g], p) if p > 0 else None) for g in range(G)])
         # dx = dz W1 + dy   (residual); with `lnprev` the input's LayerNorm backward rides in
         # the same launch (sca_gemm_lnb)
         dx = [torch.empty_like(x[g]) for g in range(G)]
-        probs = [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
+        probs = [_prob([_wseg(dz[g], W1[g], F_, d, F_, pl)], dx[g], M, d, d,
                        resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)]
         if ctx.lnprev is not None:
             hand_off(ctx.lnprev, dx, *gemm_lnb(probs, ctx.lnprev))
@@ -1561,18 +1636,19 @@ class LinearGelu(Function):
         W, b = ts[G:2 * G], ts[2 * G:3 * G]
         r = _contig(ts[3 * G:4 * G]) if has_r else [None] * G
         L.require_device(*x)
+        pl = wplanes(W)
         probs, ys, zs = [], [], []
         for g in range(G):
             n_out, n_in = W[g].shape
             M = x[g].numel() // n_in
             y = x[g].new_empty(*x[g].shape[:-1], n_out)
             z = x[g].new_empty(M, n_out)
-            probs.append(_prob([_seg(_flat(x[g]), W[g], n_in, n_in, n_in)], y, M, n_out, n_out, bias=b[g],
+            probs.append(_prob([_wseg(_flat(x[g]), W[g], n_in, n_in, n_in, pl)], y, M, n_out, n_out, bias=b[g],
                                resid=r[g], ldr=n_out, epi=L.EPI_GELU, aux_out=z, ldo=n_out))
             ys.append(y)
             zs.append(z)
         gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.has_r, ctx.b = G, has_r, tuple(b)  # biases: parameters (leaves) or None
+        ctx.G, ctx.has_r, ctx.b, ctx.pl = G, has_r, tuple(b), pl  # biases: parameters (leaves) or None
         ctx.save_for_backward(*x, *W, *zs)
         return tuple(ys)
 
@@ -1588,7 +1664,8 @@ class LinearGelu(Function):
             n_out, n_in = W[g].shape
             M = x[g].numel() // n_in
             dx = torch.empty_like(x[g])
-            probs.append(_prob([_seg(dz[g], W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
+            probs.append(_prob([_wseg(dz[g], W[g], n_out, n_in, n_out, getattr(ctx, "pl", None))], dx, M, n_in,
+                               n_in))
             dxs.append(dx)
         gemm(L.GEMM_NN, probs)
         wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
