@@ -155,6 +155,11 @@ typedef struct {
   int ldc;
   float* aux_out;
   int ldo;
+  /* optional: B's three bf16 pieces (sca_split3 planes, `bs_plane` apart, row stride ldb) —
+   * with every pass's and the main segment's planes given the launch runs on the bf16 matrix
+   * cores at fp32 accuracy (x6) */
+  const unsigned short* Bs;
+  long bs_plane;
 } sca_gemm_chain_pass;
 
 typedef struct {
@@ -170,6 +175,9 @@ typedef struct {
 
 int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                 void* stream);
+/* x6 form (gemm_ln_x6_kernel): N == 256, the main segment's B and every chained pass's B
+ * given as planes (Bs), K a positive multiple of 16, ldb and bs_plane multiples of 8, planes
+ * 16-byte aligned; otherwise the fp32 kernels run (same results to fp32 rounding).      */
 /* Row-tile height (32 or 16) sca_gemm_ln launches for nprob problems of at most maxM rows,
  * chained passes or not — the rule the launcher applies (SCA_GEMM_LN_BM overrides without
  * chained passes); hosts use it to name the kernel variant in their profiles. */

@@ -71,7 +71,8 @@ class LnBwdProblem(ctypes.Structure):
 
 class ChainPass(ctypes.Structure):
     _fields_ = [("B", c_void_p), ("ldb", c_int), ("bias", c_void_p), ("post_scale", c_float), ("epi", c_int),
-                ("C", c_void_p), ("ldc", c_int), ("aux_out", c_void_p), ("ldo", c_int)]
+                ("C", c_void_p), ("ldc", c_int), ("aux_out", c_void_p), ("ldo", c_int), ("Bs", c_void_p),
+                ("bs_plane", c_long)]
 
 
 class GemmLnProblem(ctypes.Structure):

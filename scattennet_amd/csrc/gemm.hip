@@ -1850,6 +1850,264 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #undef SCA_LN_STAMP
 }
 
+// ------------------------------------------------------------------------------ GEMM + LayerNorm, x6
+// gemm_ln_kernel<32, CH, 1> on the bf16 matrix cores (x6.h): the out-projection / fc2 of a
+// post-LN block with its weight pre-split (sca_gemm_seg.Bs) and, with CH, the chained next-op
+// passes with theirs (sca_gemm_chain_pass.Bs).  32 full rows per workgroup, 4 waves of
+// 32 x 64 (two 32x32 accumulators each), BK = 16 per slice through a 3-stage LDS-DMA ring:
+// A fp32 [32][16] (64-B rows, chunk swizzle (r >> 2) & 3), B bf16 planes [3][256][16]
+// (32-B rows, chunk swizzle (r >> 3) & 1) — the x6d images; every wave splits the 32 A rows
+// it reads (8 floats per lane per slice for 12 MFMAs).  LayerNorm epilogue as gemm_ln_kernel
+// (8 rows per wave); the chained passes read y from the LDS tile (split per fragment) and
+// their weight planes through a 2-stage ring, 16 slices per pass.
+constexpr int LX_S = 3;
+constexpr int LX_A = 32 * 16 * 4;                            // A slice (2 KiB)
+constexpr int LX_BP = LG_BN * 16 * 2;                         // one plane of a B slice (8 KiB)
+constexpr int LX_B = 3 * LX_BP;                               // 24 KiB
+constexpr int LX_STAGE = LX_A + LX_B;
+constexpr int LX_A2_OFF = 2 * LX_B;                           // chained: 2-stage B ring first
+constexpr int LX_SCR_OFF = LX_A2_OFF + 32 * LG_A2_LD * 4;
+constexpr int LX_CH_SMEM = LX_SCR_OFF + 4 * 32 * EPI_LD * 4;
+
+// per-lane source of B DMA piece q (0..23) of a [3][256][16] planes slice at k0
+__device__ __forceinline__ const unsigned short* lx_bsrc(const unsigned short* Bs, long plane, int ldb, int q,
+                                                         int lane) {
+  const int p = q >> 3, qq = q & 7;
+  const int row = 32 * qq + (lane >> 1);
+  const int ck = (lane & 1) ^ ((row >> 3) & 1);
+  return Bs + p * plane + (long)row * ldb + 8 * ck;
+}
+
+// B fragment (piece p) of rows col .. col+31 from a [3][256][16] planes image
+__device__ __forceinline__ bf16x8 lx_bfrag(const char* img, int p, int col, int lane) {
+  const int row = col + (lane & 31), h = lane >> 5;
+  return *(const bf16x8*)(img + p * LX_BP + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+}
+
+template <bool CH>
+__global__ __launch_bounds__(256) void gemm_ln_x6_kernel(const GemmLnArgs args) {
+  constexpr int S = LX_S, BM = 32, NW = 4, RPW = BM / NW;
+  constexpr int VS = LG_BN + 8;
+  constexpr int SMEM = CH ? (LX_CH_SMEM > S * LX_STAGE ? LX_CH_SMEM : S * LX_STAGE) : S * LX_STAGE;
+  static_assert(32 * VS * 4 <= S * LX_STAGE && (!CH || 32 * VS * 4 <= LX_A2_OFF), "LDS map");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  const unsigned gx = gridDim.x;
+  const unsigned nwg = gx * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * blockIdx.z;
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int pid = wgid / gx, bx = wgid % gx;
+  const sca_gemm_problem& P = args.p[pid];
+  const sca_gemm_ln_problem& LN = args.ln[pid];
+  const int m0 = bx * BM;
+  if (m0 >= P.M) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const sca_gemm_seg& G = P.seg[0];
+  const int total = G.K / 16;
+
+  // DMA: A pieces (16 rows each) by waves 0 and 1, B pieces 6w .. 6w+5
+  const bool has_a = wave < 2;
+  const float* pa;
+  {
+    const int row = 16 * (has_a ? wave : 0) + (lane >> 2);
+    const int ck = (lane & 3) ^ ((row >> 2) & 3);
+    pa = G.A + (long)min(m0 + row, P.M - 1) * G.lda + 4 * ck;
+  }
+  const unsigned short* pb[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) pb[c] = lx_bsrc(G.Bs, G.bs_plane, G.ldb, 6 * wave + c, lane);
+  auto dma = [&](int t, int stage) {
+    char* base = smem + stage * LX_STAGE;
+    if (has_a) gl_dma(pa + 16 * t, base + wave * 1024);
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      gl_dma(reinterpret_cast<const float*>(pb[c] + 16 * t), base + LX_A + (6 * wave + c) * 1024);
+  };
+
+  // the epilogue's residual rows, the bias and the LayerNorm affine: loaded before the main
+  // loop (their reads overlap it; absent residual: a harmless read of gamma)
+  const int n = 4 * lane;
+  f32x4 rin[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = min(m0 + RPW * wave + i, P.M - 1);
+    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
+  }
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero, gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < total) dma(i, i);
+  for (int t = 0; t < total; ++t) {
+    if (t + S - 2 < total) {
+      if (has_a) gl_wait_vm<7 * (S - 2)>();
+      else gl_wait_vm<6 * (S - 2)>();
+    } else {
+      gl_wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+    const char* As = smem + (t % S) * LX_STAGE;
+    const char* Bs = As + LX_A;
+    bf16x8 fb[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[j][p] = lx_bfrag(Bs, p, 64 * wave + 32 * j, lane);
+    const char* ar = As + r * 64;
+    const int sw = (r >> 2) & 3;
+    bf16x8 fa[3];
+    x6_split8(*(const f32x4*)(ar + 16 * ((2 * h) ^ sw)), *(const f32x4*)(ar + 16 * ((2 * h + 1) ^ sw)), fa);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = x6_mma(fa, fb[j], acc[j]);
+  }
+  // 32 x 256 tile -> LDS (the ring is free once every wave has passed its last slice)
+  __syncthreads();
+  float* V = reinterpret_cast<float*>(smem);
+  const float alpha = G.alpha;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      V[((q & 3) + 8 * (q >> 2) + 4 * h) * VS + 64 * wave + 32 * j + r] = acc[j][q] * alpha;
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed
+
+  DropMask dm;
+  const bool drop = (P.epi & SCA_EPI_DROPOUT) != 0;
+  if (drop) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+  const float invN = 1.0f / LG_BN;
+  f32x4 v[RPW];
+  float s[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int lr = RPW * wave + i, m = min(m0 + lr, P.M - 1);
+    f32x4 x = (ld4(&V[lr * VS + n]) + bias4) * P.post_scale;
+    if (drop) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), x[j]);
+    }
+    if (P.resid) x += rin[i];
+    v[i] = x;
+    s[i] = (x[0] + x[1]) + (x[2] + x[3]);
+  }
+  // chained passes: 16 slices of 16 k per pass, B planes through a 2-stage ring — the first
+  // two stream in under the LayerNorm math, into the V tile's region once every wave has read
+  // its rows of it
+  const int nsl = CH ? 16 * LN.npass : 0;
+  const int prot = CH && args.rot && LN.npass > 0 ? bx % LN.npass : 0;
+  auto pass_of = [&](int u) {
+    int q = (u >> 4) + prot;
+    return q >= LN.npass ? q - LN.npass : q;
+  };
+  auto dma2 = [&](int u, int stage) {
+    const sca_gemm_chain_pass& Q = LN.pass[pass_of(u)];
+    char* base = smem + stage * LX_B;
+    const long k0 = 16L * (u & 15);
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      gl_dma(reinterpret_cast<const float*>(lx_bsrc(Q.Bs, Q.bs_plane, Q.ldb, 6 * wave + c, lane) + k0),
+             base + (6 * wave + c) * 1024);
+  };
+  if constexpr (CH) {
+    __syncthreads();
+    if (nsl > 0) dma2(0, 0);
+    if (nsl > 1) dma2(1, 1);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) s[i] += __shfl_xor(s[i], o, 64);
+  float qv[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const f32x4 dv = v[i] - s[i] * invN;
+    qv[i] = (dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) qv[i] += __shfl_xor(qv[i], o, 64);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int lr = RPW * wave + i, m = m0 + lr;
+    const float mean = s[i] * invN;
+    const float rstd = 1.0f / sqrtf(qv[i] * invN + args.eps);
+    const f32x4 y = (v[i] - mean) * rstd * gam + bet;
+    if (CH) st4(reinterpret_cast<float*>(smem + LX_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
+    if (m < P.M) {
+      st4g(P.C + (long)m * P.ldc + n, v[i]);
+      st4g(LN.y + (long)m * LG_BN + n, y);
+      if (lane == 0) {
+        st1g(LN.mean + m, mean);
+        st1g(LN.rstd + m, rstd);
+      }
+    }
+  }
+  if constexpr (CH) {
+    const float* A2 = reinterpret_cast<const float*>(smem + LX_A2_OFF);
+    float* scratch = reinterpret_cast<float*>(smem + LX_SCR_OFF) + wave * 32 * EPI_LD;
+    f32x16 acc2[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
+    lds_barrier();  // every wave's y rows written to the image (its global stores stay in flight)
+    // the waits for a slice's DMA let this wave's epilogue stores stay in flight (vmcnt counts
+    // stores too, in issue order): at u = 0 the 32 LayerNorm stores (v, y, mean, rstd of 8
+    // rows) and slice 1's 6 pieces are younger than slice 0; after a pass's epilogue its 8 (16
+    // with GELU) row-piece stores.  Exact for full tiles; a partial tile waits for everything.
+    const bool full = m0 + BM <= P.M;
+    for (int u = 0; u < nsl; ++u) {
+      if (!full) {
+        gl_wait_vm<0>();
+      } else if (u == 0) {
+        if (nsl > 1) gl_wait_vm<38>();
+        else gl_wait_vm<32>();
+      } else if ((u & 15) == 0) {
+        if (LN.pass[pass_of(u - 1)].epi & SCA_EPI_GELU) gl_wait_vm<16>();
+        else gl_wait_vm<8>();
+      } else {
+        gl_wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
+      const int t = u & 15;
+      const char* Bs = smem + (u & 1) * LX_B;
+      bf16x8 fb[2][3];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[j][p] = lx_bfrag(Bs, p, 64 * wave + 32 * j, lane);
+      const float* ar = A2 + r * LG_A2_LD + 16 * t + 8 * h;
+      bf16x8 fa[3];
+      x6_split8(ld4(ar), ld4(ar + 4), fa);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc2[j] = x6_mma(fa, fb[j], acc2[j]);
+      if (t == 15) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 rows[4];
+          acc_to_rows(acc2[j], scratch, lane, rows);
+          chain_rows(LN.pass[pass_of(u)], rows, m0, P.M, 64 * wave + 32 * j, lane);
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ GEMM + LayerNorm backward
 // NN input-gradient GEMM whose epilogue runs the backward of the LayerNorm below it (the
 // post-LN block boundary, keypoint_module.py:69-72 / 105-109, walked backwards): a workgroup
@@ -2657,8 +2915,26 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
     maxM = maxM > P.M ? maxM : P.M;
   }
   if (maxM == 0) return SCA_OK;
-  const int bm = sca_gemm_ln_rows(nprob, maxM, chain);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // x6 form: every B operand given as planes
+  bool x6 = N == LG_BN;
+  auto planes_ok = [](const unsigned short* Bs, long plane, int ldb) {
+    return Bs && !(reinterpret_cast<uintptr_t>(Bs) & 15) && !(plane & 7) && !(ldb & 7);
+  };
+  for (int i = 0; i < nprob && x6; ++i) {
+    const sca_gemm_seg& S = probs[i].seg[0];
+    x6 = planes_ok(S.Bs, S.bs_plane, S.ldb) && S.K % 16 == 0;
+    for (int q = 0; q < ln[i].npass && x6; ++q) x6 = planes_ok(ln[i].pass[q].Bs, ln[i].pass[q].bs_plane, ln[i].pass[q].ldb);
+  }
+  if (x6) {
+    if (chain)
+      hipLaunchKernelGGL((gemm_ln_x6_kernel<true>), dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm_ln_x6_kernel<false>), dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
+    if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
+    return SCA_OK;
+  }
+  const int bm = sca_gemm_ln_rows(nprob, maxM, chain);
   if (N != LG_BN) {
     hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 2>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   } else if (chain) {

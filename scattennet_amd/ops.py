@@ -290,19 +290,34 @@ def _splitk_counters(n, device=None):
     return ring[pos:pos + n]
 
 
-_TILE_NAMES = {36: "gemm_tnk_kernel<3, 1, false, 0>", 37: "gemm_tnk_kernel<4, 1, false, 0>"}
+_TILE_NAMES = {36: "gemm_tnk_kernel<3, 1>", 37: "gemm_tnk_kernel<4, 1>"}
+
+
+def _kernel_name(layout, chunk, tile):
+    """The kernel a grouped launch runs, as rocprofv3 names it (mirrors pick_tile / launch_tile:
+    NT / NN with every B pre-split -> the x6 LDS-DMA kernel)."""
+    if tile:
+        return _TILE_NAMES.get(tile, f"gemm tile {tile}")
+    planes = layout != L.GEMM_TN and all(p.seg[j].Bs for p in chunk for j in range(p.nseg))
+    ok = all(p.seg[j].K % 16 == 0 for p in chunk for j in range(p.nseg)) and all(
+        p.M % 4 == 0 and p.N % (128 if layout == L.GEMM_NN else 4) == 0 for p in chunk)
+    if planes and ok:
+        tiles64 = sum(-(-p.M // 64) * -(-p.N // 64) for p in chunk)
+        return f"gemm_x6d_kernel<{layout}, 128, 128, 3>" if tiles64 // 4 >= 256 else \
+            f"gemm_x6d_kernel<{layout}, 64, 128, 3>"
+    return _GEMM_NAMES[layout]
 
 
 def gemm(layout, probs, splitk=1, ws=None, tile=0):
     """tile: a kernel variant for this call only (sca_gemm_variant ids; 0 = the heuristic),
     passed per call through the C ABI (no process-global override is touched)."""
     lib = L.lib()
-    kname = _TILE_NAMES.get(tile, f"gemm tile {tile}") if tile else _GEMM_NAMES[layout]
     st = L.stream_handle()
     for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
+        kname = _kernel_name(layout, chunk, tile) if _PROFILER else ""
         if splitk > 1 and _SPLITK_FUSED and "sca_gemm_splitk_fused" not in L.MISSING:
             cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
                                                                 max(p.N for p in chunk)),
@@ -362,7 +377,11 @@ def gemm_ln(probs, lns, eps):
         chain = any(ln.npass > 0 for ln in lchunk)
         nc = chunk[0].N // 256
         bm = 32 if nc > 1 else lib.sca_gemm_ln_rows(len(chunk), max(p.M for p in chunk), int(chain))
-        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}>", flops):
+        x6 = nc == 1 and all(p.seg[0].Bs for p in chunk) and all(ln.passes[q].Bs for ln in lchunk
+                                                                   for q in range(ln.npass))
+        kname = (f"gemm_ln_x6_kernel<{'true' if chain else 'false'}>" if x6 else
+                 f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}>")
+        with _timed(kname, flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
@@ -454,15 +473,19 @@ class NextProjections:
     def passes(self, g, M, like):
         """Producer: the ChainPass list of stream g (outputs allocated here)."""
         ps, outs = [], []
+        pl = wplanes([W for W, _, _, _ in self.specs[g]])
         for W, b, scale, gelu in self.specs[g]:
             n = W.shape[0]
             C = like.new_empty(M, n)
             A = like.new_empty(M, n) if gelu else None
+            wp = pl.get(id(W))
             for p in range(n // 256):
                 ps.append(L.ChainPass(W[256 * p:].data_ptr(), W.stride(0),
                                       b[256 * p:].data_ptr() if b is not None else None, float(scale),
                                       L.EPI_GELU if gelu else 0, C[:, 256 * p:].data_ptr(), n,
-                                      A[:, 256 * p:].data_ptr() if gelu else None, n if gelu else 0))
+                                      A[:, 256 * p:].data_ptr() if gelu else None, n if gelu else 0,
+                                      wp.ptr_for(W[256 * p:]) if wp is not None else None,
+                                      wp.plane if wp is not None else 0))
             outs.append((C, A))
         self.outs[g] = outs
         return ps
