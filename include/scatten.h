@@ -222,6 +222,12 @@ typedef struct {
    * tab = LearningPositionEmbedding.weight [>= tab_T + 2, 256], layers.py:15-30)          */
   const float* tab;
   int tab_T;
+  /* optional: wo's three bf16 pieces (sca_split3 planes, `wo_plane` apart, row stride ldw).
+   * With every segment's B given as planes (sca_gemm_seg.Bs) and, when chained, wo_s, the
+   * launch runs on the bf16 matrix cores at fp32 accuracy (x6: N == 256, K multiples of 16,
+   * ldb / ldw / planes multiples of 8); otherwise the fp32 kernels run. */
+  const unsigned short* wo_s;
+  long wo_plane;
 } sca_gemm_lnb_problem;
 
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);

@@ -83,7 +83,7 @@ class GemmLnProblem(ctypes.Structure):
 class GemmLnbProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("gamma", c_void_p), ("dx", c_void_p),
                 ("partial", c_void_p), ("wo", c_void_p), ("dout", c_void_p), ("aux", c_void_p), ("npass", c_int),
-                ("ldw", c_int), ("tab", c_void_p), ("tab_T", c_int)]
+                ("ldw", c_int), ("tab", c_void_p), ("tab_T", c_int), ("wo_s", c_void_p), ("wo_plane", c_long)]
 
 
 class PoolProblem(ctypes.Structure):

@@ -2427,6 +2427,287 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   }
 }
 
+// ------------------------------------------------------------------------------ GEMM + LayerNorm backward, x6
+// gemm_lnb_kernel<1> on the bf16 matrix cores (x6.h): the NN input-gradient GEMM of a post-LN
+// block's first op with every segment's weight pre-split (sca_gemm_seg.Bs) + the LayerNorm
+// backward of the block below, and, with `wo`, the chained dout = dx Wo (wo_s planes).  32
+// full rows per workgroup, 4 waves of 32 x 64, BK = 16 per slice through a 3-stage LDS-DMA
+// ring: A fp32 [32][16] (the x6d image), B bf16 planes k-major [3][16][256] (512-B k-rows,
+// 16-B chunk c of k-row k at c ^ (4 (k & 3)); fragments by ds_read_b64_tr_b16, conflict-free).
+constexpr int LY_S = 3;
+constexpr int LY_BP = 16 * LG_BN * 2;                        // one plane of a B slice (8 KiB)
+constexpr int LY_B = 3 * LY_BP;
+constexpr int LY_STAGE = LX_A + LY_B;
+constexpr int LY_A2_OFF = 2 * LY_B;                          // chained: 2-stage B ring first
+constexpr int LY_SCR_OFF = LY_A2_OFF + 32 * LG_A2_LD * 4;
+constexpr int LY_RED_OFF = LY_SCR_OFF + 4 * 32 * EPI_LD * 4;
+constexpr int LY_SMEM = LY_RED_OFF + 2 * 4 * LG_BN * 4;
+
+// per-lane source of B DMA piece q (0..23) of a k-major [3][16][256] planes slice at k-row k0
+// (columns n0 .. n0+255 of rows of stride ld)
+__device__ __forceinline__ const unsigned short* ly_bsrc(const unsigned short* Bs, long plane, long ld, int n0, int q,
+                                                         int lane) {
+  const int p = q >> 3, qq = q & 7;
+  const int kr = 2 * qq + (lane >> 5);
+  const int ck = (lane & 31) ^ (4 * (kr & 3));
+  return Bs + p * plane + (long)kr * ld + n0 + 8 * ck;
+}
+
+// B fragment (piece p) of columns col .. col+31 from a k-major [3][16][256] planes image
+__device__ __forceinline__ bf16x8 ly_bfrag(const char* img, int p, int col, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int kr = 8 * (g >> 1) + (i >> 2);
+  const int c = col + 16 * (g & 1) + 4 * (i & 3);
+  const char* base = img + p * LY_BP;
+  const s16x4 lo = lds_tr16(base + kr * 512 + 16 * ((c >> 3) ^ (4 * (kr & 3))) + 2 * (c & 7));
+  const s16x4 hi = lds_tr16(base + (kr + 4) * 512 + 16 * ((c >> 3) ^ (4 * ((kr + 4) & 3))) + 2 * (c & 7));
+  const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(256) void gemm_lnb_x6_kernel(const GemmLnbArgs args) {
+  if constexpr (SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
+  constexpr int S = LY_S, BM = 32, RPW = BM / 4, VS = LG_BN + 8;
+  static_assert(32 * VS * 4 <= LY_A2_OFF && S * LY_STAGE <= LY_SMEM, "LDS map");
+  __shared__ __attribute__((aligned(1024))) char smem[LY_SMEM];
+  const unsigned gx = gridDim.x;
+  const unsigned nwg = gx * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * blockIdx.z;
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int pid = wgid / gx, bx = wgid % gx;
+  const sca_gemm_problem& P = args.p[pid];
+  const sca_gemm_lnb_problem& LN = args.ln[pid];
+  const int m0 = bx * BM;
+  if (m0 >= P.M) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const bool has_a = wave < 2;
+
+  int seg_n[SCA_GEMM_MAX_SEGS];
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
+    seg_n[s] = s < P.nseg ? P.seg[s].K / 16 : 0;
+    total += seg_n[s];
+  }
+  int iseg = -1, tseg0 = 0, tend = 0;
+  const float* pa = nullptr;
+  const unsigned short* pb[6];
+  long ldb = 0;
+  auto dma = [&](int t, int stage) {
+    while (t >= tend) {
+      ++iseg;
+      tseg0 = tend;
+      tend += seg_n[iseg];
+      const sca_gemm_seg& G = P.seg[iseg];
+      const int row = 16 * (has_a ? wave : 0) + (lane >> 2);
+      const int ck = (lane & 3) ^ ((row >> 2) & 3);
+      pa = G.A + (long)min(m0 + row, P.M - 1) * G.lda + 4 * ck;
+      ldb = G.ldb;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) pb[c] = ly_bsrc(G.Bs, G.bs_plane, ldb, 0, 6 * wave + c, lane);
+    }
+    const long k0 = (long)(t - tseg0) * 16;
+    char* base = smem + stage * LY_STAGE;
+    if (has_a) gl_dma(pa + k0, base + wave * 1024);
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      gl_dma(reinterpret_cast<const float*>(pb[c] + k0 * ldb), base + LX_A + (6 * wave + c) * 1024);
+  };
+
+  // epilogue row operands (LayerNorm input, statistics, residual gradient) before the loop
+  const int n = 4 * lane;
+  f32x4 xin[RPW], rin[RPW];
+  float mu[RPW], rs[RPW];
+  const f32x4 gam = ld4(LN.gamma + n);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int m = min(m0 + RPW * wave + i, P.M - 1);
+    xin[i] = ld4(LN.x + (long)m * LG_BN + n);
+    if (LN.tab) xin[i] += ld4(LN.tab + (long)(m % LN.tab_T + 2) * LG_BN + n);  // v = x + P[t + 2]
+    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
+    mu[i] = LN.mean[m];
+    rs[i] = LN.rstd[m];
+  }
+  f32x16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < total) dma(i, i);
+  for (int t = 0; t < total; ++t) {
+    if (t + S - 2 < total) {
+      if (has_a) gl_wait_vm<7 * (S - 2)>();
+      else gl_wait_vm<6 * (S - 2)>();
+    } else {
+      gl_wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
+    const char* As = smem + (t % S) * LY_STAGE;
+    const char* Bs = As + LX_A;
+    bf16x8 fb[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[j][p] = ly_bfrag(Bs, p, 64 * wave + 32 * j, lane);
+    const char* ar = As + r * 64;
+    const int sw = (r >> 2) & 3;
+    bf16x8 fa[3];
+    x6_split8(*(const f32x4*)(ar + 16 * ((2 * h) ^ sw)), *(const f32x4*)(ar + 16 * ((2 * h + 1) ^ sw)), fa);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = x6_mma(fa, fb[j], acc[j]);
+  }
+  __syncthreads();
+  float* V = reinterpret_cast<float*>(smem);
+  const float alpha = P.seg[0].alpha;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      V[((q & 3) + 8 * (q >> 2) + 4 * h) * VS + 64 * wave + 32 * j + r] = acc[j][q] * alpha;
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed
+
+  const float invN = 1.0f / LG_BN;
+  f32x4 g[RPW], xh[RPW];
+  float s1[RPW], s2[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    g[i] = ld4(&V[(RPW * wave + i) * VS + n]);
+    if (P.resid) g[i] += rin[i];
+    xh[i] = (xin[i] - mu[i]) * rs[i];
+    const f32x4 gg = g[i] * gam;
+    s1[i] = (gg[0] + gg[1]) + (gg[2] + gg[3]);
+    const f32x4 ggx = gg * xh[i];
+    s2[i] = (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
+  }
+  // chained GEMM: its first two B slices stream in under the LayerNorm math, into the V
+  // tile's region once every wave has read its rows of it
+  const bool chain = LN.wo != nullptr;
+  const int npass = chain ? max(LN.npass, 1) : 0;
+  const long ldw = LN.ldw ? LN.ldw : (long)LG_BN * npass;
+  const unsigned short* wos = LN.wo_s;
+  const long wop = LN.wo_plane;
+  auto dma2 = [&](int u, int stage) {
+    const long k0 = 16L * (u & 15);
+    const int n0 = LG_BN * (u >> 4);
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      gl_dma(reinterpret_cast<const float*>(ly_bsrc(wos, wop, ldw, n0, 6 * wave + c, lane) + k0 * ldw),
+             smem + stage * LY_B + (6 * wave + c) * 1024);
+  };
+  if (chain) {
+    __syncthreads();
+    dma2(0, 0);
+    dma2(1, 1);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      s1[i] += __shfl_xor(s1[i], o, 64);
+      s2[i] += __shfl_xor(s2[i], o, 64);
+    }
+  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pbsum = pg;
+  float* A2 = reinterpret_cast<float*>(smem + LY_A2_OFF);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int lr = RPW * wave + i, m = m0 + lr;
+    const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rs[i];
+    if (chain) st4(A2 + lr * LG_A2_LD + n, d);  // rows past M: finite, their products never stored
+    if (m < P.M) {
+      st4g(P.C + (long)m * P.ldc + n, g[i]);
+      st4g(LN.dx + (long)m * LG_BN + n, d);
+      pg += g[i] * xh[i];
+      pbsum += g[i];
+    }
+  }
+  // the 4 waves' partial rows, summed in fixed order: dgamma, then dbeta
+  float* red = reinterpret_cast<float*>(smem + LY_RED_OFF);
+  st4(red + wave * LG_BN + n, pg);
+  st4(red + (4 + wave) * LG_BN + n, pbsum);
+  lds_barrier();
+  const long nblk = (P.M + BM - 1) / BM;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int e = threadIdx.x + 256 * c;  // (which, column) of the 2 x 256 sums
+    const int cc = e % LG_BN, which = e / LG_BN;
+    const float* rr = red + which * 4 * LG_BN + cc;
+    st1g(LN.partial + (which * nblk + bx) * LG_BN + cc, (rr[0] + rr[LG_BN]) + (rr[2 * LG_BN] + rr[3 * LG_BN]));
+  }
+  if (!chain) return;
+
+  // chained GEMM: dout[32 x 256 npass] = dx_tile[32 x 256] Wo[256 x 256 npass], 16 slices per
+  // pass; every pass's epilogue in row form through the wave's scratch
+  const bool dgelu = LN.aux != nullptr;
+  float* scratch = reinterpret_cast<float*>(smem + LY_SCR_OFF) + wave * 32 * EPI_LD;
+  f32x16 acc2[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
+  const int nsl = 16 * npass;
+  // at u = 0 the 16 row stores (g, dx of 8 rows), the 2 partial-row stores and slice 1's 6
+  // pieces are younger than slice 0; after a pass's epilogue its 8 row stores.  Exact for
+  // full tiles; a partial tile waits for everything.
+  const bool full = m0 + BM <= P.M;
+  for (int u = 0; u < nsl; ++u) {
+    if (!full) {
+      gl_wait_vm<0>();
+    } else if (u == 0) {
+      if (nsl > 1) gl_wait_vm<24>();
+      else gl_wait_vm<18>();
+    } else if ((u & 15) == 0) {
+      gl_wait_vm<8>();
+    } else {
+      gl_wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);
+    const int t = u & 15;
+    const char* Bs = smem + (u & 1) * LY_B;
+    bf16x8 fb[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[j][p] = ly_bfrag(Bs, p, 64 * wave + 32 * j, lane);
+    const float* ar = A2 + r * LG_A2_LD + 16 * t + 8 * h;
+    bf16x8 fa[3];
+    x6_split8(ld4(ar), ld4(ar + 4), fa);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc2[j] = x6_mma(fa, fb[j], acc2[j]);
+    if (t == 15) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 rows[4];
+        acc_to_rows(acc2[j], scratch, lane, rows);
+        const long cn = (long)(u >> 4) * LG_BN + 64 * wave + 32 * j + 4 * (lane & 7);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + (lane >> 3) + 8 * i;
+          if (m >= P.M) continue;
+          f32x4 o = rows[i];
+          if (dgelu) {
+            const f32x4 ax = ld4(LN.aux + (long)m * ldw + cn);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] *= gelu_erf_grad(ax[q]);
+          }
+          st4g(LN.dout + (long)m * ldw + cn, o);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
+      }
+    }
+  }
+}
+
 // Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]); bias partials likewise.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args, int nprob) {
   const sca_gemm_problem& P = args.p[blockIdx.y];
@@ -2998,6 +3279,23 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
   }
   if (maxM == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  bool x6 = N == LG_BN;  // x6 form: every B operand given as planes
+  for (int i = 0; i < nprob && x6; ++i) {
+    const sca_gemm_lnb_problem& L = lnb[i];
+    for (int s = 0; s < probs[i].nseg && x6; ++s) {
+      const sca_gemm_seg& S = probs[i].seg[s];
+      x6 = S.Bs && !(reinterpret_cast<uintptr_t>(S.Bs) & 15) && !(S.bs_plane & 7) && !(S.ldb & 7) && S.K % 16 == 0;
+    }
+    if (L.wo) {
+      const long ldw = L.ldw ? L.ldw : (long)LG_BN * (L.npass ? L.npass : 1);
+      x6 = x6 && L.wo_s && !(reinterpret_cast<uintptr_t>(L.wo_s) & 15) && !(L.wo_plane & 7) && !(ldw & 7);
+    }
+  }
+  if (x6) {
+    hipLaunchKernelGGL(gemm_lnb_x6_kernel, dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
+    if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }
+    return SCA_OK;
+  }
   if (N == LG_BN) hipLaunchKernelGGL(gemm_lnb_kernel<1>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   else hipLaunchKernelGGL(gemm_lnb_kernel<2>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }

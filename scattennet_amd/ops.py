@@ -547,16 +547,23 @@ def gemm_lnb(probs, lnp):
     n2 = lnp[0].wo.shape[1] if chain else 0
     dout = [o.v.new_empty(*o.v.shape[:-1], n2) for o in lnp] if chain else [None] * len(lnp)
     arr = (L.GemmProblem * len(probs))(*probs)
+    wpl = wplanes([o.wo for o in lnp]) if chain else {}
+
+    def wo_planes(o):
+        p = wpl.get(id(o.wo))
+        return (p.ptr_for(o.wo), p.plane) if p is not None else (None, 0)
     larr = (L.GemmLnbProblem * len(lnp))(*[L.GemmLnbProblem(o.v.data_ptr(), o.mean.data_ptr(), o.rstd.data_ptr(),
                                                            o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr(),
                                                            ptr(o.wo) if chain else None, ptr(dout[g]),
                                                            ptr(o.aux) if chain else None, n2 // 256, n2,
-                                                           ptr(o.tab), o.T)
+                                                           ptr(o.tab), o.T, *wo_planes(o))
                                             for g, o in enumerate(lnp)])
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
-    with _timed(f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
+    x6 = probs[0].N == 256 and all(p.seg[j].Bs for p in probs for j in range(p.nseg)) and (
+        not chain or all(pl is not None for pl in wpl.values()))
+    with _timed("gemm_lnb_x6_kernel" if x6 else f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
 
