@@ -39,6 +39,10 @@ class LaunchProfiler:
             st["launches"] += 1
         return out
 
+    def launches(self, *prefixes):
+        """Launch count of the kernels whose names start with any of `prefixes`."""
+        return sum(v["launches"] for k, v in self.stats().items() if k.startswith(prefixes))
+
     def dominant(self):
         st = self.stats()
         k = max(st, key=lambda n: st[n]["seconds"])
@@ -64,6 +68,10 @@ class _timed:
             self.e1.record()
             _PROFILER.records.append((self.key, self.flops, self.e0, self.e1))
 
+
+# name prefixes of every kernel that can run a layout's plain GEMM (tests count launches by them)
+GEMM_KERNELS = {lay: (f"gemm_glds_kernel<{lay},", f"gemm_x6d_kernel<{lay},", f"gemm_x6_kernel<{lay},",
+                      f"gemm_kernel<{lay}") for lay in range(3)}
 
 # rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>:
 # the ring depth pick_tile chooses, 3 stages forward, 2 for the gradient layouts)
@@ -117,7 +125,28 @@ class Planes:
 # forward pass and the NT / NN GEMMs that read them run the x6 LDS-DMA kernel.  False: every
 # GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32) — the same results to fp32 rounding.
 X6 = True
+# which launch families take the planes (tools/gemm_ln_bench.py, bench.py --x6): the plain
+# NT / NN GEMMs, the GEMM + LayerNorm forward, its backward
+X6_KINDS = {"gemm": True, "ln": False, "lnb": False}
 _PLANES = None  # id(weight) -> Planes inside a weight_planes scope
+
+
+def set_x6(kinds):
+    """kinds: iterable of "gemm" / "ln" / "lnb" (the others run the fp32 kernels)."""
+    kinds = set(kinds)
+    for k in X6_KINDS:
+        X6_KINDS[k] = k in kinds
+
+
+def _strip_planes(probs, lns=None, lnbs=None):
+    for p in probs:
+        for j in range(p.nseg):
+            p.seg[j].Bs, p.seg[j].bs_plane = None, 0
+    for ln in lns or ():
+        for q in range(ln.npass):
+            ln.passes[q].Bs, ln.passes[q].bs_plane = None, 0
+    for o in lnbs or ():
+        o.wo_s, o.wo_plane = None, 0
 
 
 class weight_planes:
@@ -316,8 +345,10 @@ def gemm(layout, probs, splitk=1, ws=None, tile=0):
     for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
+        if not X6_KINDS["gemm"]:
+            _strip_planes(arr)
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
-        kname = _kernel_name(layout, chunk, tile) if _PROFILER else ""
+        kname = _kernel_name(layout, list(arr), tile) if _PROFILER else ""
         if splitk > 1 and _SPLITK_FUSED and "sca_gemm_splitk_fused" not in L.MISSING:
             cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
                                                                 max(p.N for p in chunk)),
@@ -371,6 +402,9 @@ def gemm_ln(probs, lns, eps):
         chunk, lchunk = probs[i:i + L.GEMM_LN_MAX_PROBLEMS], lns[i:i + L.GEMM_LN_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
         larr = (L.GemmLnProblem * len(lchunk))(*lchunk)
+        if not X6_KINDS["ln"]:
+            _strip_planes(arr, larr)
+            chunk, lchunk = list(arr), list(larr)
         flops = sum(2.0 * p.M * p.N * (p.seg[0].K + 256 * ln.npass) for p, ln in zip(chunk, lchunk)) \
             if _PROFILER else 0.0
         # the variant sca_gemm_ln picks, for the kernel name rocprofv3 shows
@@ -561,8 +595,10 @@ def gemm_lnb(probs, lnp):
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
-    x6 = probs[0].N == 256 and all(p.seg[j].Bs for p in probs for j in range(p.nseg)) and (
-        not chain or all(pl is not None for pl in wpl.values()))
+    if not X6_KINDS["lnb"]:
+        _strip_planes(arr, lnbs=larr)
+    x6 = probs[0].N == 256 and all(p.seg[j].Bs for p in arr for j in range(p.nseg)) and (
+        not chain or all(o.wo_s for o in larr))
     with _timed("gemm_lnb_x6_kernel" if x6 else f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout

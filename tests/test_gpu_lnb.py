@@ -200,10 +200,10 @@ def test_chained_blocks_hand_off_layer_norm_backward(second_consumer, dz, monkey
     torch.cuda.synchronize()
     # hand-offs: block 1's FFN -> its attention LN; block 1's attention -> block 0's last LN;
     # block 0's FFN -> its attention LN (block 0's attention input x has no fused producer)
-    assert prof.stats().get("gemm_lnb_kernel<1>", {}).get("launches", 0) == 3
+    assert prof.launches("gemm_lnb_kernel<1>", "gemm_lnb_x6_kernel") == 3
     # NN launches: block 0's attention dX (no fused producer), block 1's FFN dz (its output has
     # no fused consumer) and block 0's FFN dz unless block 1's launch chained it
-    nn = prof.stats().get(ops._GEMM_NAMES[L.GEMM_NN], {}).get("launches", 0)
+    nn = prof.launches(*ops.GEMM_KERNELS[L.GEMM_NN])
     assert nn == (2 if dz and not second_consumer else 3), nn
 
     ps = [{k: v.detach().cpu().clone().requires_grad_(True) for k, v in blk.state_dict().items()} for blk in blocks]
