@@ -50,9 +50,6 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one captured hipGraph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--x6", default=None,
-                    help="comma list of launch families on the x6 kernels: gemm, ln, lnb (default: ops.X6_KINDS); "
-                         "'none' = every GEMM on the fp32 matrix cores")
     ap.add_argument("--dropout", type=float, default=0.0,
                     help="train-mode dropout p for every block (the yaml's 0.2 = the secondary run)")
     return ap.parse_args()
@@ -77,8 +74,6 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     w = W.WORKLOADS[args.workload]
-    if args.x6 is not None:
-        ops.set_x6([] if args.x6 == "none" else args.x6.split(","))
 
     fusion = bool(w.get("fusion"))
     model = W.build_encoder(w, dev, seed=0) if fusion else W.build_streams(w, dev, seed=0, init="reference")

@@ -78,11 +78,6 @@ typedef struct {
   int K;       /* reduction length of this segment (any: K, lda, ldb not multiples of 4 or
                   operands not 16-byte aligned take the element-wise load form) */
   float alpha; /* scales A on load: alpha=0.5 reproduces v_proj(kv/2) exactly */
-  /* optional: B already split into its three bf16 pieces by sca_split3 (planes of B's own
-   * layout and leading dimension ldb, `bs_plane` elements apart), read instead of B by the
-   * x6 kernels (NT / NN); NULL = B is split inside the GEMM */
-  const unsigned short* Bs;
-  long bs_plane;
 } sca_gemm_seg;
 
 typedef struct {
@@ -155,11 +150,6 @@ typedef struct {
   int ldc;
   float* aux_out;
   int ldo;
-  /* optional: B's three bf16 pieces (sca_split3 planes, `bs_plane` apart, row stride ldb) —
-   * with every pass's and the main segment's planes given the launch runs on the bf16 matrix
-   * cores at fp32 accuracy (x6) */
-  const unsigned short* Bs;
-  long bs_plane;
 } sca_gemm_chain_pass;
 
 typedef struct {
@@ -175,9 +165,6 @@ typedef struct {
 
 int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_problem* ln, float eps,
                 void* stream);
-/* x6 form (gemm_ln_x6_kernel): N == 256, the main segment's B and every chained pass's B
- * given as planes (Bs), K a positive multiple of 16, ldb and bs_plane multiples of 8, planes
- * 16-byte aligned; otherwise the fp32 kernels run (same results to fp32 rounding).      */
 /* Row-tile height (32 or 16) sca_gemm_ln launches for nprob problems of at most maxM rows,
  * chained passes or not — the rule the launcher applies (SCA_GEMM_LN_BM overrides without
  * chained passes); hosts use it to name the kernel variant in their profiles. */
@@ -222,29 +209,10 @@ typedef struct {
    * tab = LearningPositionEmbedding.weight [>= tab_T + 2, 256], layers.py:15-30)          */
   const float* tab;
   int tab_T;
-  /* optional: wo's three bf16 pieces (sca_split3 planes, `wo_plane` apart, row stride ldw).
-   * With every segment's B given as planes (sca_gemm_seg.Bs) and, when chained, wo_s, the
-   * launch runs on the bf16 matrix cores at fp32 accuracy (x6: N == 256, K multiples of 16,
-   * ldb / ldw / planes multiples of 8); otherwise the fp32 kernels run. */
-  const unsigned short* wo_s;
-  long wo_plane;
 } sca_gemm_lnb_problem;
 
 int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_gemm_lnb_problem* lnb, void* stream);
 int sca_gemm_lnb_blocks(int M);
-
-/* fp32 -> the three bf16 pieces of the x6 GEMMs (include/scatten.h, sca_gemm_seg.Bs):
- * dst[p * plane + i] = piece p of src[i], x = hi + mid + lo (round to nearest at each step;
- * the residual is below 2^-24 |x|).  One launch over up to SCA_SPLIT_MAX_PROBLEMS arrays —
- * every Linear weight of a step at once.                                                  */
-typedef struct {
-  const float* src;
-  unsigned short* dst;
-  long n;     /* elements */
-  long plane; /* elements between dst's planes (>= n) */
-} sca_split_problem;
-#define SCA_SPLIT_MAX_PROBLEMS 64
-int sca_split3(int nprob, const sca_split_problem* probs, void* stream);
 
 /* Tuning knob: force the kernel variant of one layout for every later sca_gemm* call
  * (0 = built-in heuristic; 1 / 5 / 7 register-staged 64x64 / single-buffered 64x64 /

@@ -27,13 +27,11 @@ POOL_MAX_PROBLEMS = 8
 SOFTMAX_MAX_PROBLEMS = 8
 GELU_MAX_PROBLEMS = 8
 DROPOUT_MAX_PROBLEMS = 12
-SPLIT_MAX_PROBLEMS = 64
 ACT_NONE, ACT_RELU = 0, 1
 
 
 class GemmSeg(ctypes.Structure):
-    _fields_ = [("A", c_void_p), ("B", c_void_p), ("lda", c_int), ("ldb", c_int), ("K", c_int), ("alpha", c_float),
-                ("Bs", c_void_p), ("bs_plane", c_long)]
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("lda", c_int), ("ldb", c_int), ("K", c_int), ("alpha", c_float)]
 
 
 class GemmProblem(ctypes.Structure):
@@ -71,8 +69,7 @@ class LnBwdProblem(ctypes.Structure):
 
 class ChainPass(ctypes.Structure):
     _fields_ = [("B", c_void_p), ("ldb", c_int), ("bias", c_void_p), ("post_scale", c_float), ("epi", c_int),
-                ("C", c_void_p), ("ldc", c_int), ("aux_out", c_void_p), ("ldo", c_int), ("Bs", c_void_p),
-                ("bs_plane", c_long)]
+                ("C", c_void_p), ("ldc", c_int), ("aux_out", c_void_p), ("ldo", c_int)]
 
 
 class GemmLnProblem(ctypes.Structure):
@@ -83,7 +80,7 @@ class GemmLnProblem(ctypes.Structure):
 class GemmLnbProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("gamma", c_void_p), ("dx", c_void_p),
                 ("partial", c_void_p), ("wo", c_void_p), ("dout", c_void_p), ("aux", c_void_p), ("npass", c_int),
-                ("ldw", c_int), ("tab", c_void_p), ("tab_T", c_int), ("wo_s", c_void_p), ("wo_plane", c_long)]
+                ("ldw", c_int), ("tab", c_void_p), ("tab_T", c_int)]
 
 
 class PoolProblem(ctypes.Structure):
@@ -100,10 +97,6 @@ class GeluBwdProblem(ctypes.Structure):
 
 class DropoutProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("seed", c_u64)]
-
-
-class SplitProblem(ctypes.Structure):
-    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("n", c_long), ("plane", c_long)]
 
 
 class ReduceProblem(ctypes.Structure):
@@ -130,7 +123,6 @@ EXPORTS = {
     "sca_gemm_splitk_fused": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_variant": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
-    "sca_split3": ([c_int, c_void_p, c_void_p], c_int),
     "sca_gemm_ln_rows": ([c_int, c_int, c_int], c_int),
     "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_lnb_blocks": ([c_int], c_int),

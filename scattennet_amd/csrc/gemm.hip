@@ -21,7 +21,6 @@
 // Numerics: exact f32 products, f32 accumulation (the MFMA is a k-ordered fmaf chain);
 // summation order differs from ATen's, so results match the reference to ~1e-6 relative.
 #include "common.h"
-#include "x6.h"
 #include "../../include/scatten.h"
 
 namespace {
@@ -431,8 +430,6 @@ constexpr int GL_OP_BYTES = GL_BM * GL_BK * 4;  // 8 KiB per operand per stage
 
 __device__ __forceinline__ int gl_swz(int row) { return (row >> 1) & 7; }
 
-// (a global_load_lds builtin given a non-float source pointer silently drops the host launch
-// stubs of the kernels using it — bf16 sources go through this float* form)
 __device__ __forceinline__ void gl_dma(const float* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -927,537 +924,6 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 }
 
-// ------------------------------------------------------------------------------ x6 GEMM
-// Grouped GEMM on the bf16 matrix cores with fp32 accuracy (x6.h): the default kernel of
-// every layout.  BM x BN tile, 4 waves (2 x 2, each (BM/2) x (BN/2) as 32x32 blocks), K in
-// BK slices.  A slice of each operand is loaded to registers (float4, coalesced), split
-// into its three bf16 pieces and written to a double-buffered LDS image [piece][row][BK]
-// (k-contiguous rows of BK bf16 + 16 B pad: the 32x32x16 fragment reads, one ds_read_b128
-// per piece, are conflict-free); the next slice's loads are in flight during the current
-// slice's MFMAs.  k-major operands (B of NN, A and B of TN) are loaded as 4 k x 4 row
-// blocks and transposed in registers, so both orientations build the same image.
-// Epilogue, split-K (slabs, or combined in-launch by the last arriving split) and the fused
-// TN bias column sums as gemm_glds_kernel.  Requirements (x6_ok): every segment's K per
-// split-K chunk a multiple of BK, M, N multiples of 4, one alpha per problem, float4 loads
-// (vec_ok).
-template <int ROWS, int BK>
-struct X6Img {
-  static constexpr int PITCH = BK * 2 + 16;  // bytes per row
-  static constexpr int PIECE = ROWS * PITCH;
-  static constexpr int BYTES = 3 * PIECE;
-};
-
-template <bool KC, int ROWS, int BK>
-struct X6Stage {
-  static constexpr int NV = KC ? ROWS * BK / 4 / 256 : 0;  // float4 per thread (KC)
-  static constexpr int NB = KC ? 0 : ROWS * BK / 16;        // 4 k x 4 row blocks (k-major)
-  static constexpr int NBT = KC ? 0 : (NB + 255) / 256;     // blocks per thread
-  static constexpr int NREG = KC ? NV : 4 * NBT;
-  static_assert(!KC || NV * 1024 == ROWS * BK, "tile not divisible among 256 threads");
-  f32x4 v[NREG];
-
-  // KC: element (row, k) at base[row * ld + k], else at base[k * ld + row]; rows past
-  // `nrows` are clamped (never stored)
-  __device__ __forceinline__ void load(const float* base, int ld, int r0, int nrows, int k0) {
-    if constexpr (KC) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int e = threadIdx.x + i * 256;
-        const int row = e / (BK / 4), kq = e % (BK / 4);
-        v[i] = ld4(base + (long)min(r0 + row, nrows - 1) * ld + k0 + 4 * kq);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NBT; ++i) {
-        const int b = threadIdx.x + i * 256;
-        if (NB % 256 == 0 || b < NB) {
-          const int kq = b % (BK / 4), rq = b / (BK / 4);
-          const float* p = base + (long)(k0 + 4 * kq) * ld + min(r0 + 4 * rq, nrows - 4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[4 * i + j] = ld4(p + (long)j * ld);
-        }
-      }
-    }
-  }
-  __device__ __forceinline__ void store(char* img) const {
-    using I = X6Img<ROWS, BK>;
-    if constexpr (KC) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int e = threadIdx.x + i * 256;
-        const int row = e / (BK / 4), kq = e % (BK / 4);
-        uint2 h, m, l;
-        x6_split4(v[i], h, m, l);
-        char* p = img + row * I::PITCH + kq * 8;
-        *(uint2*)(p) = h;
-        *(uint2*)(p + I::PIECE) = m;
-        *(uint2*)(p + 2 * I::PIECE) = l;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NBT; ++i) {
-        const int b = threadIdx.x + i * 256;
-        if (NB % 256 == 0 || b < NB) {
-          const int kq = b % (BK / 4), rq = b / (BK / 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const f32x4 t = {v[4 * i][r], v[4 * i + 1][r], v[4 * i + 2][r], v[4 * i + 3][r]};
-            uint2 h, m, l;
-            x6_split4(t, h, m, l);
-            char* p = img + (4 * rq + r) * I::PITCH + kq * 8;
-            *(uint2*)(p) = h;
-            *(uint2*)(p + I::PIECE) = m;
-            *(uint2*)(p + 2 * I::PIECE) = l;
-          }
-        }
-      }
-    }
-  }
-  // k-major only: this thread's partial column sums of its 4 rows (TN bias gradient)
-  __device__ __forceinline__ void colsum(f32x4& s) const {
-    if constexpr (!KC) {
-      const int b = threadIdx.x;
-      if (NB % 256 == 0 || b < NB) s += (v[0] + v[1]) + (v[2] + v[3]);
-    }
-  }
-};
-
-// x6 kernels' epilogue (after the main loop; the LDS ring is free): alpha, then per 32x32
-// block the row-form epilogue (epilogue_rows), a split-K slab, or the in-launch combine of
-// gemm_glds_kernel (write-through slabs + ticket, the last arriver sums in slice order and,
-// with do_bias, the TN bias partials that the caller stored for rows m0 .. m0 + bias_rows).
-template <int RM, int RN>
-__device__ __forceinline__ void x6_epilogue(const GemmArgs& args, const sca_gemm_problem& P, f32x16 (&acc)[RM][RN],
-                                            int pid, int ks, int splitk, int mw, int nw, unsigned gx, unsigned gy,
-                                            int bx, int by, char* smem, bool do_bias, int m0, int bias_rows) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float alpha = P.seg[0].alpha;
-  const bool fused_k = splitk > 1 && args.counters != nullptr;
-  __syncthreads();  // every wave is past its last slice: the ring is free
-  if (alpha != 1.f) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] *= alpha;
-  }
-  // the ring is free: wave-private transposition scratch for the row-form epilogue
-  float* scratch = reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD;
-  if (!fused_k) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        f32x4 rows[4];
-        acc_to_rows(acc[i][j], scratch, lane, rows);
-        if (splitk > 1)
-          slab_rows(args.ws + args.slab_off[pid] + (long)ks * P.M * P.N, rows, P.M, P.N, mw + 32 * i,
-                    nw + 32 * j, lane);
-        else
-          epilogue_rows(P, rows, mw + 32 * i, nw + 32 * j, lane, args.drop_off);
-        __builtin_amdgcn_wave_barrier();  // the scratch is reused by the next block
-      }
-    return;
-  }
-  const long MN = (long)P.M * P.N;
-  float* slabs = args.ws + args.slab_off[pid];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      f32x4 rows[4];
-      acc_to_rows(acc[i][j], scratch, lane, rows);
-      slab_rows_sc1(slabs, (long)splitk * MN, rows, P.M, P.N, mw + 32 * i, nw + 32 * j, lane,
-                    (long)ks * MN);
-      __builtin_amdgcn_wave_barrier();
-    }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  unsigned* flag = reinterpret_cast<unsigned*>(smem + 4 * 32 * EPI_LD * 4);
-  unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
-  if (threadIdx.x == 0)
-    *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
-  __syncthreads();
-  if (!*flag) return;
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded: no agent acquire
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int mb = mw + 32 * i, nb = nw + 32 * j;
-      const int n = nb + 4 * (lane & 7);
-      f32x4 rows[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = min(mb + (lane >> 3) + 8 * q, P.M - 1);
-        const long e = (long)m * P.N + min(n, P.N - 4);
-        f32x4 tt = ld4_sc1(rs, e);
-        for (int s2 = 1; s2 < splitk; ++s2) tt += ld4_sc1(rs, s2 * MN + e);
-        rows[q] = tt;
-      }
-      epilogue_rows(P, rows, mb, nb, lane, args.drop_off);
-    }
-  if (do_bias && threadIdx.x < bias_rows && m0 + (int)threadIdx.x < P.M) {
-    float* bp = args.ws + args.bias_off[pid] + m0 + threadIdx.x;
-    float tt = 0.f;
-    for (int s2 = 0; s2 < splitk; ++s2)
-      tt += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    P.bias_grad[m0 + threadIdx.x] = tt * P.bias_grad_scale;
-  }
-}
-
-
-template <int LAYOUT, int BM, int BN, int BK>
-__global__ __launch_bounds__(256) void gemm_x6_kernel(const GemmArgs args) {
-  if constexpr (LAYOUT == SCA_GEMM_NN && SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
-  constexpr bool A_KC = (LAYOUT != SCA_GEMM_TN);
-  constexpr bool B_KC = (LAYOUT == SCA_GEMM_NT);
-  using IA = X6Img<BM, BK>;
-  using IB = X6Img<BN, BK>;
-  constexpr int STAGE = IA::BYTES + IB::BYTES;
-  constexpr int RM = BM / 64, RN = BN / 64;
-  static_assert(2 * STAGE >= 4 * 32 * EPI_LD * 4 + 64, "epilogue scratch fits the ring");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  const unsigned gx = gridDim.x, gy = gridDim.y;
-  const unsigned nwg = gx * gy * gridDim.z;
-  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
-
-  const int splitk = args.splitk;
-  const int pid = bz / splitk;
-  const int ks = bz % splitk;
-  const sca_gemm_problem& P = args.p[pid];
-  const int m0 = by * BM, n0 = bx * BN;
-  if (m0 >= P.M || n0 >= P.N) return;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
-  const int r = lane & 31, h = lane >> 5;
-
-  // flattened (segment, K-slice) sequence; every chunk a whole number of slices
-  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
-  int total = 0;
-#pragma unroll
-  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
-    seg_kbeg[s] = seg_n[s] = 0;
-    if (s < P.nseg) {
-      int kbeg = 0, kend = P.seg[s].K;
-      if (splitk > 1) {
-        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + BK - 1) / BK * BK;
-        kbeg = ks * chunk;
-        kend = min(P.seg[s].K, kbeg + chunk);
-      }
-      seg_kbeg[s] = kbeg;
-      seg_n[s] = kend > kbeg ? (kend - kbeg) / BK : 0;
-      total += seg_n[s];
-    }
-  }
-  X6Stage<A_KC, BM, BK> sa;
-  X6Stage<B_KC, BN, BK> sb;
-  int iseg = -1, tseg0 = 0, tend = 0;
-  auto load = [&](int t) {
-    while (t >= tend) {
-      ++iseg;
-      tseg0 = tend;
-      tend += seg_n[iseg];
-    }
-    const sca_gemm_seg& G = P.seg[iseg];
-    const int k0 = seg_kbeg[iseg] + (t - tseg0) * BK;
-    sa.load(G.A, G.lda, m0, P.M, k0);
-    sb.load(G.B, G.ldb, n0, P.N, k0);
-  };
-
-  const bool do_bias = (LAYOUT == SCA_GEMM_TN) && P.bias_grad != nullptr && bx == 0;
-  f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
-  f32x16 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-
-  if (total > 0) {
-    load(0);
-    if (do_bias) sa.colsum(bs4);
-    sa.store(smem);
-    sb.store(smem + IA::BYTES);
-  }
-  __syncthreads();
-  for (int t = 0; t < total; ++t) {
-    const char* st = smem + (t & 1) * STAGE;
-    if (t + 1 < total) load(t + 1);  // in flight during this slice's MFMAs
-#pragma unroll
-    for (int kk = 0; kk < BK / 16; ++kk) {
-      bf16x8 fa[RM][3], fb[RN][3];
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fa[i][p] = *(const bf16x8*)(st + p * IA::PIECE + (wm + 32 * i + r) * IA::PITCH + 32 * kk + 16 * h);
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fb[j][p] = *(const bf16x8*)(st + IA::BYTES + p * IB::PIECE + (wn + 32 * j + r) * IB::PITCH + 32 * kk + 16 * h);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) acc[i][j] = x6_mma(fa[i], fb[j], acc[i][j]);
-    }
-    if (t + 1 < total) {
-      char* nx = smem + ((t + 1) & 1) * STAGE;
-      if (do_bias) sa.colsum(bs4);
-      sa.store(nx);
-      sb.store(nx + IA::BYTES);
-    }
-    __syncthreads();
-  }
-
-  const float alpha = P.seg[0].alpha;
-  const bool fused_k = splitk > 1 && args.counters != nullptr;  // in-launch split-K combine
-  // bias gradient (TN): the threads sharing a row quad (BK/4 consecutive lanes) sum their
-  // k-partials; the first of them owns rows 4 rq .. 4 rq + 3 of the tile
-  if (do_bias) {
-#pragma unroll
-    for (int o = 1; o < BK / 4; o <<= 1)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bs4[q] += __shfl_xor(bs4[q], o, 64);
-    constexpr int NB = BM * BK / 16;
-    const int b = threadIdx.x, rq = b / (BK / 4);
-    if ((NB % 256 == 0 || b < NB) && b % (BK / 4) == 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = m0 + 4 * rq + q;
-        if (m >= P.M) continue;
-        float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m;
-        if (fused_k)
-          __hip_atomic_store(bp, bs4[q] * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
-        else if (splitk > 1)
-          *bp = bs4[q] * alpha;
-        else
-          P.bias_grad[m] = bs4[q] * alpha * P.bias_grad_scale;
-      }
-    }
-  }
-  x6_epilogue<RM, RN>(args, P, acc, pid, ks, splitk, m0 + wm, n0 + wn, gx, gy, bx, by, smem, do_bias, m0, BM);
-}
-
-// ------------------------------------------------------------------------------ x6, LDS-DMA
-// The x6 GEMM for NT / NN launches whose B operands (the Linear weights) come pre-split
-// (sca_gemm_seg.Bs, sca_split3): both operands stream through an S-stage LDS ring by
-// global_load_lds (no VGPR staging, no ds_write pass), BK = 16 per slice.
-//   A (fp32, k-contiguous [BM][16], 64-B rows): 16-B chunk c of row r at c ^ ((r >> 2) & 3)
-//     (source-address swizzle; the two ds_read_b128 of a 32x32x16 fragment are
-//     conflict-free); each wave splits its own A fragments in registers (8 floats per lane
-//     per 32-row block and k-step: 36 VALU for 6 x (RN) MFMAs).
-//   B planes, NT (k-contiguous [3][BN][16] bf16, 32-B rows): chunk c of row r at
-//     c ^ ((r >> 3) & 1); one ds_read_b128 per piece and block.
-//   B planes, NN (k-major [3][16][BN] bf16, 2*BN-B rows, BN = 128): 16-B chunk c of k-row
-//     k at c ^ (4 (k & 3)); fragments by two ds_read_b64_tr_b16 per piece and block (the
-//     hardware transpose, cdna_hip_programming.md T10) — conflict-free with that swizzle.
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ s16x4 lds_tr16(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
-}
-
-// eight floats -> three bf16x8 fragments
-__device__ __forceinline__ void x6_split8(f32x4 a, f32x4 b, bf16x8 (&f)[3]) {
-  uint4 h, m, l;
-  x6_split2(a[0], a[1], h.x, m.x, l.x);
-  x6_split2(a[2], a[3], h.y, m.y, l.y);
-  x6_split2(b[0], b[1], h.z, m.z, l.z);
-  x6_split2(b[2], b[3], h.w, m.w, l.w);
-  f[0] = __builtin_bit_cast(bf16x8, h);
-  f[1] = __builtin_bit_cast(bf16x8, m);
-  f[2] = __builtin_bit_cast(bf16x8, l);
-}
-
-template <int LAYOUT, int BM, int BN, int S>
-__global__ __launch_bounds__(256) void gemm_x6d_kernel(const GemmArgs args) {
-  static_assert(LAYOUT == SCA_GEMM_NT || (LAYOUT == SCA_GEMM_NN && BN == 128), "x6d: NT, or NN at BN = 128");
-  if constexpr (LAYOUT == SCA_GEMM_NN && SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
-  constexpr int BK = 16;
-  constexpr int A_BYTES = BM * BK * 4;          // fp32 [BM][16]
-  constexpr int B_PIECE = BN * BK * 2;          // one bf16 plane of the slice
-  constexpr int B_BYTES = 3 * B_PIECE;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int A_DMA = A_BYTES / 1024 / 4;     // DMA pieces per wave per slice
-  constexpr int B_DMA = B_BYTES / 1024 / 4;
-  static_assert(A_DMA * 4096 == A_BYTES && B_DMA * 4096 == B_BYTES, "whole DMA pieces per wave");
-  constexpr int RM = BM / 64, RN = BN / 64;
-  constexpr int SMEM = S * STAGE > 4 * 32 * EPI_LD * 4 + 64 ? S * STAGE : 4 * 32 * EPI_LD * 4 + 64;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-  const unsigned gx = gridDim.x, gy = gridDim.y;
-  const unsigned nwg = gx * gy * gridDim.z;
-  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
-  const int splitk = args.splitk;
-  const int pid = bz / splitk;
-  const int ks = bz % splitk;
-  const sca_gemm_problem& P = args.p[pid];
-  const int m0 = by * BM, n0 = bx * BN;
-  if (m0 >= P.M || n0 >= P.N) return;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
-  const int r = lane & 31, h = lane >> 5;
-
-  int seg_kbeg[SCA_GEMM_MAX_SEGS], seg_n[SCA_GEMM_MAX_SEGS];
-  int total = 0;
-#pragma unroll
-  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
-    seg_kbeg[s] = seg_n[s] = 0;
-    if (s < P.nseg) {
-      int kbeg = 0, kend = P.seg[s].K;
-      if (splitk > 1) {
-        const int chunk = ((P.seg[s].K + splitk - 1) / splitk + BK - 1) / BK * BK;
-        kbeg = ks * chunk;
-        kend = min(P.seg[s].K, kbeg + chunk);
-      }
-      seg_kbeg[s] = kbeg;
-      seg_n[s] = kend > kbeg ? (kend - kbeg) / BK : 0;
-      total += seg_n[s];
-    }
-  }
-  // per-lane DMA sources at the first slice of the segment being issued + per-slice steps
-  int iseg = -1, tseg0 = 0, tend = 0;
-  const float* pa[A_DMA];
-  const unsigned short* pb[B_DMA];
-  long stepB = 0;
-  auto dma = [&](int t, int stage) {
-    while (t >= tend) {
-      ++iseg;
-      tseg0 = tend;
-      tend += seg_n[iseg];
-      const sca_gemm_seg& G = P.seg[iseg];
-      const int kb = seg_kbeg[iseg];
-#pragma unroll
-      for (int c = 0; c < A_DMA; ++c) {  // piece q = 16 rows of 64 B
-        const int q = wave * A_DMA + c;
-        const int row = 16 * q + (lane >> 2);
-        const int ck = (lane & 3) ^ ((row >> 2) & 3);
-        pa[c] = G.A + (long)min(m0 + row, P.M - 1) * G.lda + kb + 4 * ck;
-      }
-#pragma unroll
-      for (int c = 0; c < B_DMA; ++c) {
-        const int q = wave * B_DMA + c;
-        constexpr int PPP = B_PIECE / 1024;  // DMA pieces per plane
-        const int plane = q / PPP, qq = q % PPP;
-        if constexpr (LAYOUT == SCA_GEMM_NT) {  // 32 rows of 32 B per DMA piece
-          const int row = 32 * qq + (lane >> 1);
-          const int ck = (lane & 1) ^ ((row >> 3) & 1);
-          pb[c] = G.Bs + plane * G.bs_plane + (long)min(n0 + row, P.N - 1) * G.ldb + kb + 8 * ck;
-        } else {  // 4 k-rows of 256 B per DMA piece
-          const int kr = 4 * qq + (lane >> 4);
-          const int ck = (lane & 15) ^ (4 * (kr & 3));
-          pb[c] = G.Bs + plane * G.bs_plane + (long)(kb + kr) * G.ldb + n0 + 8 * ck;
-        }
-      }
-      stepB = LAYOUT == SCA_GEMM_NT ? BK : (long)BK * G.ldb;
-    }
-    const long kk = t - tseg0;
-    char* base = smem + stage * STAGE;
-#pragma unroll
-    for (int c = 0; c < A_DMA; ++c) gl_dma(pa[c] + kk * BK, base + (wave * A_DMA + c) * 1024);
-#pragma unroll
-    for (int c = 0; c < B_DMA; ++c)
-      gl_dma(reinterpret_cast<const float*>(pb[c] + kk * stepB), base + A_BYTES + (wave * B_DMA + c) * 1024);
-  };
-
-  f32x16 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < total) dma(i, i);
-  constexpr int PER = A_DMA + B_DMA;  // DMA instructions per wave per slice
-  for (int t = 0; t < total; ++t) {
-    if (t + S - 2 < total) gl_wait_vm<PER * (S - 2)>();
-    else gl_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t-1's stage fully read
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
-    const char* As = smem + (t % S) * STAGE;
-    const char* Bs = As + A_BYTES;
-    bf16x8 fb[RN][3];
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = wn + 32 * j;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        if constexpr (LAYOUT == SCA_GEMM_NT) {
-          const int row = col + r;
-          fb[j][p] = *(const bf16x8*)(Bs + p * B_PIECE + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
-        } else {
-          // lane 16g + i: k-rows 8 (g >> 1) + q (+4), columns col + 16 (g & 1) + 4 (i & 3) .. +3
-          const int g = lane >> 4, i = lane & 15;
-          const int kr = 8 * (g >> 1) + (i >> 2);
-          const int c = col + 16 * (g & 1) + 4 * (i & 3);
-          const char* base = Bs + p * B_PIECE;
-          const s16x4 lo = lds_tr16(base + kr * 256 + 16 * ((c >> 3) ^ (4 * (kr & 3))) + 2 * (c & 7));
-          const s16x4 hi = lds_tr16(base + (kr + 4) * 256 + 16 * ((c >> 3) ^ (4 * ((kr + 4) & 3))) + 2 * (c & 7));
-          const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          fb[j][p] = __builtin_bit_cast(bf16x8, v);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int row = wm + 32 * i + r;
-      const char* ar = As + row * 64;
-      const int sw = (row >> 2) & 3;
-      bf16x8 fa[3];
-      x6_split8(*(const f32x4*)(ar + 16 * ((2 * h) ^ sw)), *(const f32x4*)(ar + 16 * ((2 * h + 1) ^ sw)), fa);
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = x6_mma(fa, fb[j], acc[i][j]);
-    }
-  }
-  x6_epilogue<RM, RN>(args, P, acc, pid, ks, splitk, m0 + wm, n0 + wn, gx, gy, bx, by, smem, false, m0, BM);
-}
-
-
-// ------------------------------------------------------------------------------ split3
-// fp32 -> three bf16 planes (x6.h): 4 elements per thread per step, grid-stride over the
-// concatenation of the problems (blockIdx.y = problem)
-struct SplitArgs {
-  sca_split_problem p[SCA_SPLIT_MAX_PROBLEMS];
-};
-
-__global__ __launch_bounds__(256) void split3_kernel(const SplitArgs args) {
-  const sca_split_problem& P = args.p[blockIdx.y];
-  const long n4 = P.n >> 2;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n4; e += (long)gridDim.x * 256) {
-    uint2 h, m, l;
-    x6_split4(ld4(P.src + 4 * e), h, m, l);
-    *(uint2*)(P.dst + 4 * e) = h;
-    *(uint2*)(P.dst + P.plane + 4 * e) = m;
-    *(uint2*)(P.dst + 2 * P.plane + 4 * e) = l;
-  }
-  const long tail = (long)blockIdx.x * 256 + threadIdx.x;
-  if (tail < (P.n & 3)) {  // the last n % 4 elements
-    const long i = 4 * n4 + tail;
-    unsigned hh, mm, ll;
-    x6_split2(P.src[i], 0.f, hh, mm, ll);
-    P.dst[i] = (unsigned short)hh;
-    P.dst[P.plane + i] = (unsigned short)mm;
-    P.dst[2 * P.plane + i] = (unsigned short)ll;
-  }
-}
-
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -1850,264 +1316,6 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #undef SCA_LN_STAMP
 }
 
-// ------------------------------------------------------------------------------ GEMM + LayerNorm, x6
-// gemm_ln_kernel<32, CH, 1> on the bf16 matrix cores (x6.h): the out-projection / fc2 of a
-// post-LN block with its weight pre-split (sca_gemm_seg.Bs) and, with CH, the chained next-op
-// passes with theirs (sca_gemm_chain_pass.Bs).  32 full rows per workgroup, 4 waves of
-// 32 x 64 (two 32x32 accumulators each), BK = 16 per slice through a 3-stage LDS-DMA ring:
-// A fp32 [32][16] (64-B rows, chunk swizzle (r >> 2) & 3), B bf16 planes [3][256][16]
-// (32-B rows, chunk swizzle (r >> 3) & 1) — the x6d images; every wave splits the 32 A rows
-// it reads (8 floats per lane per slice for 12 MFMAs).  LayerNorm epilogue as gemm_ln_kernel
-// (8 rows per wave); the chained passes read y from the LDS tile (split per fragment) and
-// their weight planes through a 2-stage ring, 16 slices per pass.
-constexpr int LX_S = 3;
-constexpr int LX_A = 32 * 16 * 4;                            // A slice (2 KiB)
-constexpr int LX_BP = LG_BN * 16 * 2;                         // one plane of a B slice (8 KiB)
-constexpr int LX_B = 3 * LX_BP;                               // 24 KiB
-constexpr int LX_STAGE = LX_A + LX_B;
-constexpr int LX_A2_OFF = 2 * LX_B;                           // chained: 2-stage B ring first
-constexpr int LX_SCR_OFF = LX_A2_OFF + 32 * LG_A2_LD * 4;
-constexpr int LX_CH_SMEM = LX_SCR_OFF + 4 * 32 * EPI_LD * 4;
-
-// per-lane source of B DMA piece q (0..23) of a [3][256][16] planes slice at k0
-__device__ __forceinline__ const unsigned short* lx_bsrc(const unsigned short* Bs, long plane, int ldb, int q,
-                                                         int lane) {
-  const int p = q >> 3, qq = q & 7;
-  const int row = 32 * qq + (lane >> 1);
-  const int ck = (lane & 1) ^ ((row >> 3) & 1);
-  return Bs + p * plane + (long)row * ldb + 8 * ck;
-}
-
-// B fragment (piece p) of rows col .. col+31 from a [3][256][16] planes image
-__device__ __forceinline__ bf16x8 lx_bfrag(const char* img, int p, int col, int lane) {
-  const int row = col + (lane & 31), h = lane >> 5;
-  return *(const bf16x8*)(img + p * LX_BP + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
-}
-
-template <bool CH>
-__global__ __launch_bounds__(256) void gemm_ln_x6_kernel(const GemmLnArgs args) {
-  constexpr int S = LX_S, BM = 32, NW = 4, RPW = BM / NW;
-  constexpr int VS = LG_BN + 8;
-  constexpr int SMEM = CH ? (LX_CH_SMEM > S * LX_STAGE ? LX_CH_SMEM : S * LX_STAGE) : S * LX_STAGE;
-  static_assert(32 * VS * 4 <= S * LX_STAGE && (!CH || 32 * VS * 4 <= LX_A2_OFF), "LDS map");
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-  const unsigned gx = gridDim.x;
-  const unsigned nwg = gx * gridDim.z;
-  const unsigned orig = blockIdx.x + gx * blockIdx.z;
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int pid = wgid / gx, bx = wgid % gx;
-  const sca_gemm_problem& P = args.p[pid];
-  const sca_gemm_ln_problem& LN = args.ln[pid];
-  const int m0 = bx * BM;
-  if (m0 >= P.M) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const sca_gemm_seg& G = P.seg[0];
-  const int total = G.K / 16;
-
-  // DMA: A pieces (16 rows each) by waves 0 and 1, B pieces 6w .. 6w+5
-  const bool has_a = wave < 2;
-  const float* pa;
-  {
-    const int row = 16 * (has_a ? wave : 0) + (lane >> 2);
-    const int ck = (lane & 3) ^ ((row >> 2) & 3);
-    pa = G.A + (long)min(m0 + row, P.M - 1) * G.lda + 4 * ck;
-  }
-  const unsigned short* pb[6];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) pb[c] = lx_bsrc(G.Bs, G.bs_plane, G.ldb, 6 * wave + c, lane);
-  auto dma = [&](int t, int stage) {
-    char* base = smem + stage * LX_STAGE;
-    if (has_a) gl_dma(pa + 16 * t, base + wave * 1024);
-#pragma unroll
-    for (int c = 0; c < 6; ++c)
-      gl_dma(reinterpret_cast<const float*>(pb[c] + 16 * t), base + LX_A + (6 * wave + c) * 1024);
-  };
-
-  // the epilogue's residual rows, the bias and the LayerNorm affine: loaded before the main
-  // loop (their reads overlap it; absent residual: a harmless read of gamma)
-  const int n = 4 * lane;
-  f32x4 rin[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int m = min(m0 + RPW * wave + i, P.M - 1);
-    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
-  }
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 bias4 = P.bias ? ld4(P.bias + n) : zero, gam = ld4(LN.gamma + n), bet = ld4(LN.beta + n);
-
-  f32x16 acc[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < total) dma(i, i);
-  for (int t = 0; t < total; ++t) {
-    if (t + S - 2 < total) {
-      if (has_a) gl_wait_vm<7 * (S - 2)>();
-      else gl_wait_vm<6 * (S - 2)>();
-    } else {
-      gl_wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
-    const char* As = smem + (t % S) * LX_STAGE;
-    const char* Bs = As + LX_A;
-    bf16x8 fb[2][3];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fb[j][p] = lx_bfrag(Bs, p, 64 * wave + 32 * j, lane);
-    const char* ar = As + r * 64;
-    const int sw = (r >> 2) & 3;
-    bf16x8 fa[3];
-    x6_split8(*(const f32x4*)(ar + 16 * ((2 * h) ^ sw)), *(const f32x4*)(ar + 16 * ((2 * h + 1) ^ sw)), fa);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[j] = x6_mma(fa, fb[j], acc[j]);
-  }
-  // 32 x 256 tile -> LDS (the ring is free once every wave has passed its last slice)
-  __syncthreads();
-  float* V = reinterpret_cast<float*>(smem);
-  const float alpha = G.alpha;
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      V[((q & 3) + 8 * (q >> 2) + 4 * h) * VS + 64 * wave + 32 * j + r] = acc[j][q] * alpha;
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed
-
-  DropMask dm;
-  const bool drop = (P.epi & SCA_EPI_DROPOUT) != 0;
-  if (drop) dm.init(P.drop_seed, P.drop_p, args.drop_off);
-  const float invN = 1.0f / LG_BN;
-  f32x4 v[RPW];
-  float s[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int lr = RPW * wave + i, m = min(m0 + lr, P.M - 1);
-    f32x4 x = (ld4(&V[lr * VS + n]) + bias4) * P.post_scale;
-    if (drop) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), x[j]);
-    }
-    if (P.resid) x += rin[i];
-    v[i] = x;
-    s[i] = (x[0] + x[1]) + (x[2] + x[3]);
-  }
-  // chained passes: 16 slices of 16 k per pass, B planes through a 2-stage ring — the first
-  // two stream in under the LayerNorm math, into the V tile's region once every wave has read
-  // its rows of it
-  const int nsl = CH ? 16 * LN.npass : 0;
-  const int prot = CH && args.rot && LN.npass > 0 ? bx % LN.npass : 0;
-  auto pass_of = [&](int u) {
-    int q = (u >> 4) + prot;
-    return q >= LN.npass ? q - LN.npass : q;
-  };
-  auto dma2 = [&](int u, int stage) {
-    const sca_gemm_chain_pass& Q = LN.pass[pass_of(u)];
-    char* base = smem + stage * LX_B;
-    const long k0 = 16L * (u & 15);
-#pragma unroll
-    for (int c = 0; c < 6; ++c)
-      gl_dma(reinterpret_cast<const float*>(lx_bsrc(Q.Bs, Q.bs_plane, Q.ldb, 6 * wave + c, lane) + k0),
-             base + (6 * wave + c) * 1024);
-  };
-  if constexpr (CH) {
-    __syncthreads();
-    if (nsl > 0) dma2(0, 0);
-    if (nsl > 1) dma2(1, 1);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) s[i] += __shfl_xor(s[i], o, 64);
-  float qv[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const f32x4 dv = v[i] - s[i] * invN;
-    qv[i] = (dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) qv[i] += __shfl_xor(qv[i], o, 64);
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int lr = RPW * wave + i, m = m0 + lr;
-    const float mean = s[i] * invN;
-    const float rstd = 1.0f / sqrtf(qv[i] * invN + args.eps);
-    const f32x4 y = (v[i] - mean) * rstd * gam + bet;
-    if (CH) st4(reinterpret_cast<float*>(smem + LX_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
-    if (m < P.M) {
-      st4g(P.C + (long)m * P.ldc + n, v[i]);
-      st4g(LN.y + (long)m * LG_BN + n, y);
-      if (lane == 0) {
-        st1g(LN.mean + m, mean);
-        st1g(LN.rstd + m, rstd);
-      }
-    }
-  }
-  if constexpr (CH) {
-    const float* A2 = reinterpret_cast<const float*>(smem + LX_A2_OFF);
-    float* scratch = reinterpret_cast<float*>(smem + LX_SCR_OFF) + wave * 32 * EPI_LD;
-    f32x16 acc2[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
-    lds_barrier();  // every wave's y rows written to the image (its global stores stay in flight)
-    // the waits for a slice's DMA let this wave's epilogue stores stay in flight (vmcnt counts
-    // stores too, in issue order): at u = 0 the 32 LayerNorm stores (v, y, mean, rstd of 8
-    // rows) and slice 1's 6 pieces are younger than slice 0; after a pass's epilogue its 8 (16
-    // with GELU) row-piece stores.  Exact for full tiles; a partial tile waits for everything.
-    const bool full = m0 + BM <= P.M;
-    for (int u = 0; u < nsl; ++u) {
-      if (!full) {
-        gl_wait_vm<0>();
-      } else if (u == 0) {
-        if (nsl > 1) gl_wait_vm<38>();
-        else gl_wait_vm<32>();
-      } else if ((u & 15) == 0) {
-        if (LN.pass[pass_of(u - 1)].epi & SCA_EPI_GELU) gl_wait_vm<16>();
-        else gl_wait_vm<8>();
-      } else {
-        gl_wait_vm<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
-      const int t = u & 15;
-      const char* Bs = smem + (u & 1) * LX_B;
-      bf16x8 fb[2][3];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) fb[j][p] = lx_bfrag(Bs, p, 64 * wave + 32 * j, lane);
-      const float* ar = A2 + r * LG_A2_LD + 16 * t + 8 * h;
-      bf16x8 fa[3];
-      x6_split8(ld4(ar), ld4(ar + 4), fa);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc2[j] = x6_mma(fa, fb[j], acc2[j]);
-      if (t == 15) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x4 rows[4];
-          acc_to_rows(acc2[j], scratch, lane, rows);
-          chain_rows(LN.pass[pass_of(u)], rows, m0, P.M, 64 * wave + 32 * j, lane);
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
-        }
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------ GEMM + LayerNorm backward
 // NN input-gradient GEMM whose epilogue runs the backward of the LayerNorm below it (the
 // post-LN block boundary, keypoint_module.py:69-72 / 105-109, walked backwards): a workgroup
@@ -2427,287 +1635,6 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   }
 }
 
-// ------------------------------------------------------------------------------ GEMM + LayerNorm backward, x6
-// gemm_lnb_kernel<1> on the bf16 matrix cores (x6.h): the NN input-gradient GEMM of a post-LN
-// block's first op with every segment's weight pre-split (sca_gemm_seg.Bs) + the LayerNorm
-// backward of the block below, and, with `wo`, the chained dout = dx Wo (wo_s planes).  32
-// full rows per workgroup, 4 waves of 32 x 64, BK = 16 per slice through a 3-stage LDS-DMA
-// ring: A fp32 [32][16] (the x6d image), B bf16 planes k-major [3][16][256] (512-B k-rows,
-// 16-B chunk c of k-row k at c ^ (4 (k & 3)); fragments by ds_read_b64_tr_b16, conflict-free).
-constexpr int LY_S = 3;
-constexpr int LY_BP = 16 * LG_BN * 2;                        // one plane of a B slice (8 KiB)
-constexpr int LY_B = 3 * LY_BP;
-constexpr int LY_STAGE = LX_A + LY_B;
-constexpr int LY_A2_OFF = 2 * LY_B;                          // chained: 2-stage B ring first
-constexpr int LY_SCR_OFF = LY_A2_OFF + 32 * LG_A2_LD * 4;
-constexpr int LY_RED_OFF = LY_SCR_OFF + 4 * 32 * EPI_LD * 4;
-constexpr int LY_SMEM = LY_RED_OFF + 2 * 4 * LG_BN * 4;
-
-// per-lane source of B DMA piece q (0..23) of a k-major [3][16][256] planes slice at k-row k0
-// (columns n0 .. n0+255 of rows of stride ld)
-__device__ __forceinline__ const unsigned short* ly_bsrc(const unsigned short* Bs, long plane, long ld, int n0, int q,
-                                                         int lane) {
-  const int p = q >> 3, qq = q & 7;
-  const int kr = 2 * qq + (lane >> 5);
-  const int ck = (lane & 31) ^ (4 * (kr & 3));
-  return Bs + p * plane + (long)kr * ld + n0 + 8 * ck;
-}
-
-// B fragment (piece p) of columns col .. col+31 from a k-major [3][16][256] planes image
-__device__ __forceinline__ bf16x8 ly_bfrag(const char* img, int p, int col, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int kr = 8 * (g >> 1) + (i >> 2);
-  const int c = col + 16 * (g & 1) + 4 * (i & 3);
-  const char* base = img + p * LY_BP;
-  const s16x4 lo = lds_tr16(base + kr * 512 + 16 * ((c >> 3) ^ (4 * (kr & 3))) + 2 * (c & 7));
-  const s16x4 hi = lds_tr16(base + (kr + 4) * 512 + 16 * ((c >> 3) ^ (4 * ((kr + 4) & 3))) + 2 * (c & 7));
-  const short __attribute__((ext_vector_type(8))) v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-__global__ __launch_bounds__(256) void gemm_lnb_x6_kernel(const GemmLnbArgs args) {
-  if constexpr (SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
-  constexpr int S = LY_S, BM = 32, RPW = BM / 4, VS = LG_BN + 8;
-  static_assert(32 * VS * 4 <= LY_A2_OFF && S * LY_STAGE <= LY_SMEM, "LDS map");
-  __shared__ __attribute__((aligned(1024))) char smem[LY_SMEM];
-  const unsigned gx = gridDim.x;
-  const unsigned nwg = gx * gridDim.z;
-  const unsigned orig = blockIdx.x + gx * blockIdx.z;
-  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int pid = wgid / gx, bx = wgid % gx;
-  const sca_gemm_problem& P = args.p[pid];
-  const sca_gemm_lnb_problem& LN = args.ln[pid];
-  const int m0 = bx * BM;
-  if (m0 >= P.M) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const bool has_a = wave < 2;
-
-  int seg_n[SCA_GEMM_MAX_SEGS];
-  int total = 0;
-#pragma unroll
-  for (int s = 0; s < SCA_GEMM_MAX_SEGS; ++s) {
-    seg_n[s] = s < P.nseg ? P.seg[s].K / 16 : 0;
-    total += seg_n[s];
-  }
-  int iseg = -1, tseg0 = 0, tend = 0;
-  const float* pa = nullptr;
-  const unsigned short* pb[6];
-  long ldb = 0;
-  auto dma = [&](int t, int stage) {
-    while (t >= tend) {
-      ++iseg;
-      tseg0 = tend;
-      tend += seg_n[iseg];
-      const sca_gemm_seg& G = P.seg[iseg];
-      const int row = 16 * (has_a ? wave : 0) + (lane >> 2);
-      const int ck = (lane & 3) ^ ((row >> 2) & 3);
-      pa = G.A + (long)min(m0 + row, P.M - 1) * G.lda + 4 * ck;
-      ldb = G.ldb;
-#pragma unroll
-      for (int c = 0; c < 6; ++c) pb[c] = ly_bsrc(G.Bs, G.bs_plane, ldb, 0, 6 * wave + c, lane);
-    }
-    const long k0 = (long)(t - tseg0) * 16;
-    char* base = smem + stage * LY_STAGE;
-    if (has_a) gl_dma(pa + k0, base + wave * 1024);
-#pragma unroll
-    for (int c = 0; c < 6; ++c)
-      gl_dma(reinterpret_cast<const float*>(pb[c] + k0 * ldb), base + LX_A + (6 * wave + c) * 1024);
-  };
-
-  // epilogue row operands (LayerNorm input, statistics, residual gradient) before the loop
-  const int n = 4 * lane;
-  f32x4 xin[RPW], rin[RPW];
-  float mu[RPW], rs[RPW];
-  const f32x4 gam = ld4(LN.gamma + n);
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int m = min(m0 + RPW * wave + i, P.M - 1);
-    xin[i] = ld4(LN.x + (long)m * LG_BN + n);
-    if (LN.tab) xin[i] += ld4(LN.tab + (long)(m % LN.tab_T + 2) * LG_BN + n);  // v = x + P[t + 2]
-    rin[i] = ld4((P.resid ? P.resid + (long)m * P.ldr : LN.gamma) + n);
-    mu[i] = LN.mean[m];
-    rs[i] = LN.rstd[m];
-  }
-  f32x16 acc[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < total) dma(i, i);
-  for (int t = 0; t < total; ++t) {
-    if (t + S - 2 < total) {
-      if (has_a) gl_wait_vm<7 * (S - 2)>();
-      else gl_wait_vm<6 * (S - 2)>();
-    } else {
-      gl_wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + S - 1 < total) dma(t + S - 1, (t + S - 1) % S);
-    const char* As = smem + (t % S) * LY_STAGE;
-    const char* Bs = As + LX_A;
-    bf16x8 fb[2][3];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fb[j][p] = ly_bfrag(Bs, p, 64 * wave + 32 * j, lane);
-    const char* ar = As + r * 64;
-    const int sw = (r >> 2) & 3;
-    bf16x8 fa[3];
-    x6_split8(*(const f32x4*)(ar + 16 * ((2 * h) ^ sw)), *(const f32x4*)(ar + 16 * ((2 * h + 1) ^ sw)), fa);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[j] = x6_mma(fa, fb[j], acc[j]);
-  }
-  __syncthreads();
-  float* V = reinterpret_cast<float*>(smem);
-  const float alpha = P.seg[0].alpha;
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      V[((q & 3) + 8 * (q >> 2) + 4 * h) * VS + 64 * wave + 32 * j + r] = acc[j][q] * alpha;
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed
-
-  const float invN = 1.0f / LG_BN;
-  f32x4 g[RPW], xh[RPW];
-  float s1[RPW], s2[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    g[i] = ld4(&V[(RPW * wave + i) * VS + n]);
-    if (P.resid) g[i] += rin[i];
-    xh[i] = (xin[i] - mu[i]) * rs[i];
-    const f32x4 gg = g[i] * gam;
-    s1[i] = (gg[0] + gg[1]) + (gg[2] + gg[3]);
-    const f32x4 ggx = gg * xh[i];
-    s2[i] = (ggx[0] + ggx[1]) + (ggx[2] + ggx[3]);
-  }
-  // chained GEMM: its first two B slices stream in under the LayerNorm math, into the V
-  // tile's region once every wave has read its rows of it
-  const bool chain = LN.wo != nullptr;
-  const int npass = chain ? max(LN.npass, 1) : 0;
-  const long ldw = LN.ldw ? LN.ldw : (long)LG_BN * npass;
-  const unsigned short* wos = LN.wo_s;
-  const long wop = LN.wo_plane;
-  auto dma2 = [&](int u, int stage) {
-    const long k0 = 16L * (u & 15);
-    const int n0 = LG_BN * (u >> 4);
-#pragma unroll
-    for (int c = 0; c < 6; ++c)
-      gl_dma(reinterpret_cast<const float*>(ly_bsrc(wos, wop, ldw, n0, 6 * wave + c, lane) + k0 * ldw),
-             smem + stage * LY_B + (6 * wave + c) * 1024);
-  };
-  if (chain) {
-    __syncthreads();
-    dma2(0, 0);
-    dma2(1, 1);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      s1[i] += __shfl_xor(s1[i], o, 64);
-      s2[i] += __shfl_xor(s2[i], o, 64);
-    }
-  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pbsum = pg;
-  float* A2 = reinterpret_cast<float*>(smem + LY_A2_OFF);
-#pragma unroll
-  for (int i = 0; i < RPW; ++i) {
-    const int lr = RPW * wave + i, m = m0 + lr;
-    const f32x4 d = (g[i] * gam - s1[i] * invN - xh[i] * (s2[i] * invN)) * rs[i];
-    if (chain) st4(A2 + lr * LG_A2_LD + n, d);  // rows past M: finite, their products never stored
-    if (m < P.M) {
-      st4g(P.C + (long)m * P.ldc + n, g[i]);
-      st4g(LN.dx + (long)m * LG_BN + n, d);
-      pg += g[i] * xh[i];
-      pbsum += g[i];
-    }
-  }
-  // the 4 waves' partial rows, summed in fixed order: dgamma, then dbeta
-  float* red = reinterpret_cast<float*>(smem + LY_RED_OFF);
-  st4(red + wave * LG_BN + n, pg);
-  st4(red + (4 + wave) * LG_BN + n, pbsum);
-  lds_barrier();
-  const long nblk = (P.M + BM - 1) / BM;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int e = threadIdx.x + 256 * c;  // (which, column) of the 2 x 256 sums
-    const int cc = e % LG_BN, which = e / LG_BN;
-    const float* rr = red + which * 4 * LG_BN + cc;
-    st1g(LN.partial + (which * nblk + bx) * LG_BN + cc, (rr[0] + rr[LG_BN]) + (rr[2 * LG_BN] + rr[3 * LG_BN]));
-  }
-  if (!chain) return;
-
-  // chained GEMM: dout[32 x 256 npass] = dx_tile[32 x 256] Wo[256 x 256 npass], 16 slices per
-  // pass; every pass's epilogue in row form through the wave's scratch
-  const bool dgelu = LN.aux != nullptr;
-  float* scratch = reinterpret_cast<float*>(smem + LY_SCR_OFF) + wave * 32 * EPI_LD;
-  f32x16 acc2[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
-  const int nsl = 16 * npass;
-  // at u = 0 the 16 row stores (g, dx of 8 rows), the 2 partial-row stores and slice 1's 6
-  // pieces are younger than slice 0; after a pass's epilogue its 8 row stores.  Exact for
-  // full tiles; a partial tile waits for everything.
-  const bool full = m0 + BM <= P.M;
-  for (int u = 0; u < nsl; ++u) {
-    if (!full) {
-      gl_wait_vm<0>();
-    } else if (u == 0) {
-      if (nsl > 1) gl_wait_vm<24>();
-      else gl_wait_vm<18>();
-    } else if ((u & 15) == 0) {
-      gl_wait_vm<8>();
-    } else {
-      gl_wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);
-    const int t = u & 15;
-    const char* Bs = smem + (u & 1) * LY_B;
-    bf16x8 fb[2][3];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fb[j][p] = ly_bfrag(Bs, p, 64 * wave + 32 * j, lane);
-    const float* ar = A2 + r * LG_A2_LD + 16 * t + 8 * h;
-    bf16x8 fa[3];
-    x6_split8(ld4(ar), ld4(ar + 4), fa);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc2[j] = x6_mma(fa, fb[j], acc2[j]);
-    if (t == 15) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x4 rows[4];
-        acc_to_rows(acc2[j], scratch, lane, rows);
-        const long cn = (long)(u >> 4) * LG_BN + 64 * wave + 32 * j + 4 * (lane & 7);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + (lane >> 3) + 8 * i;
-          if (m >= P.M) continue;
-          f32x4 o = rows[i];
-          if (dgelu) {
-            const f32x4 ax = ld4(LN.aux + (long)m * ldw + cn);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] *= gelu_erf_grad(ax[q]);
-          }
-          st4g(LN.dout + (long)m * ldw + cn, o);
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc2[j][q] = 0.f;
-      }
-    }
-  }
-}
-
 // Fixed-order split-K reduction + epilogue: C = epi(sum_s slab[s]); bias partials likewise.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args, int nprob) {
   const sca_gemm_problem& P = args.p[blockIdx.y];
@@ -2771,10 +1698,6 @@ int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
 //   7  register-staged 128x64, 8 waves (NN fallback)
 //   20 / 21 / 22  LDS-DMA 64x64 with a 3- / 2- / 4-stage ring (the heuristic's kernels)
 //   36 / 37  TN only: the k-split outer-product weight-gradient kernel, 3- / 4-stage ring
-//   50 .. 56  x6 (bf16 matrix cores, fp32 accuracy): BM x BN x BK = 128x128x16, 128x64x32,
-//      64x128x32, 64x64x32, 128x128x32, 128x64x16, 64x64x16
-//   60 .. 63  x6 over LDS-DMA, NT / NN with pre-split B (sca_gemm_seg.Bs): BM x BN = 128x128
-//      with a 3- / 4-stage ring, 64x128 with 3 / 4 stages
 using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
 using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
 using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
@@ -2784,8 +1707,6 @@ bool valid_tile(int layout, int tile) {
   switch (tile) {
     case 0: case 1: case 5: case 7: case 20: case 21: case 22: return true;
     case 36: case 37: return layout == SCA_GEMM_TN;
-    case 50: case 51: case 52: case 53: case 54: case 55: case 56: return true;
-    case 60: case 61: case 62: case 63: return layout != SCA_GEMM_TN;
     default: return false;
   }
 }
@@ -2829,46 +1750,6 @@ int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-template <int LAYOUT, int BM, int BN, int BK>
-int launch_x6(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  dim3 grid((maxN + BN - 1) / BN, (maxM + BM - 1) / BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_x6_kernel<LAYOUT, BM, BN, BK>), grid, dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
-}
-
-// the x6 kernels' shape requirements: the LDS-DMA kernel's (K per chunk a multiple of BK)
-bool x6_ok(const GemmArgs& a, int nprob, int bk) {
-  for (int i = 0; i < nprob; ++i) {
-    const sca_gemm_problem& P = a.p[i];
-    if ((P.M & 3) || (P.N & 3)) return false;
-    for (int s = 0; s < P.nseg; ++s)
-      if ((P.seg[s].K % bk) || P.seg[s].alpha != P.seg[0].alpha) return false;
-  }
-  return true;
-}
-
-template <int LAYOUT, int BM, int BN, int S>
-int launch_x6d(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  dim3 grid((maxN + BN - 1) / BN, (maxM + BM - 1) / BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_x6d_kernel<LAYOUT, BM, BN, S>), grid, dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
-}
-
-// gemm_x6d_kernel: every segment's B pre-split (16-B aligned planes, rows of a multiple of 8
-// bf16), K per chunk a multiple of 16; NN needs N a multiple of 128 (whole k-major B rows)
-bool x6d_ok(const GemmArgs& a, int nprob, int layout) {
-  if (layout == SCA_GEMM_TN || !x6_ok(a, nprob, 16)) return false;
-  for (int i = 0; i < nprob; ++i) {
-    const sca_gemm_problem& P = a.p[i];
-    if (layout == SCA_GEMM_NN && (P.N % 128)) return false;
-    for (int s = 0; s < P.nseg; ++s) {
-      const sca_gemm_seg& G = P.seg[s];
-      if (!G.Bs || (reinterpret_cast<uintptr_t>(G.Bs) & 15) || (G.ldb & 7) || (G.bs_plane & 7)) return false;
-    }
-  }
-  return true;
-}
-
 bool tn_ok(const GemmArgs& a, int nprob) {
   for (int i = 0; i < nprob; ++i)
     if (a.p[i].nseg != 1) return false;
@@ -2882,30 +1763,6 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
     if (LAYOUT == SCA_GEMM_TN && tn_ok(a, nprob))
       return tile == 36 ? launch_tnk<3, 1>(a, nprob, maxM, maxN, st) : launch_tnk<4, 1>(a, nprob, maxM, maxN, st);
     tile = 21;
-  }
-  if (tile >= 60) {
-    if (x6d_ok(a, nprob, LAYOUT)) {
-      if constexpr (LAYOUT != SCA_GEMM_TN) switch (tile) {
-          case 60: return launch_x6d<LAYOUT, 128, 128, 3>(a, nprob, maxM, maxN, st);
-          case 61: return launch_x6d<LAYOUT, 128, 128, 4>(a, nprob, maxM, maxN, st);
-          case 62: return launch_x6d<LAYOUT, 64, 128, 3>(a, nprob, maxM, maxN, st);
-          default: return launch_x6d<LAYOUT, 64, 128, 4>(a, nprob, maxM, maxN, st);
-        }
-    }
-    tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;  // not eligible (e.g. no pre-split B): fp32 kernels
-  }
-  if (tile >= 50) {
-    const int bk = (tile == 50 || tile == 55 || tile == 56) ? 16 : 32;
-    if (x6_ok(a, nprob, bk)) switch (tile) {
-        case 50: return launch_x6<LAYOUT, 128, 128, 16>(a, nprob, maxM, maxN, st);
-        case 51: return launch_x6<LAYOUT, 128, 64, 32>(a, nprob, maxM, maxN, st);
-        case 52: return launch_x6<LAYOUT, 64, 128, 32>(a, nprob, maxM, maxN, st);
-        case 53: return launch_x6<LAYOUT, 64, 64, 32>(a, nprob, maxM, maxN, st);
-        case 54: return launch_x6<LAYOUT, 128, 128, 32>(a, nprob, maxM, maxN, st);
-        case 55: return launch_x6<LAYOUT, 128, 64, 16>(a, nprob, maxM, maxN, st);
-        default: return launch_x6<LAYOUT, 64, 64, 16>(a, nprob, maxM, maxN, st);
-      }
-    tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;
   }
   if (tile >= 20 && !glds_ok(a, nprob)) tile = LAYOUT == SCA_GEMM_TN ? 5 : (LAYOUT == SCA_GEMM_NN ? 7 : 1);
   switch (tile) {
@@ -2923,14 +1780,11 @@ int g_tile_override[3] = {0, 0, 0};
 // Tile heuristic (measured with tools/gemm_bench.py at the workload's shapes, see
 // DESIGN.md): the 3-stage LDS-DMA 64x64 kernel wins every layout; ineligible shapes fall
 // back to 64x64 / 4 waves (NT), 128x64 / 8 waves (NN), single-buffered 64x64 (TN).
-int pick_tile(int layout, long tiles64, int splitk, bool planes) {
+int pick_tile(int layout, long tiles64, int splitk) {
   if (g_tile_override[layout]) return g_tile_override[layout];
   (void)splitk;
-  // NT / NN with pre-split weights: the x6 LDS-DMA kernel, 128x128 tiles when they still
-  // cover the 256 CUs, else 64x128 (launch_tile falls back to the fp32 kernels when a shape
-  // is not eligible)
-  if (planes && layout != SCA_GEMM_TN) return tiles64 / 4 >= 256 ? 60 : 62;
-  // LDS-DMA fp32 kernel; launch_tile falls back per layout when a shape is not eligible.  The
+  (void)tiles64;
+  // LDS-DMA kernel; launch_tile falls back per layout when a shape is not eligible.  The
   // input- and weight-gradient layouts use the 2-stage ring (32 KB: up to 5 workgroups / CU
   // beside the concurrent streams' kernels; bench.py A/B +0.9 %), the forward 3 stages.
   return layout == SCA_GEMM_NT ? 20 : 21;
@@ -3029,14 +1883,10 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   int rc;
   long tiles64 = 0;
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
-  bool planes = layout != SCA_GEMM_TN;
-  for (int i = 0; i < nprob; ++i)
-    for (int sg = 0; sg < probs[i].nseg; ++sg) planes = planes && probs[i].seg[sg].Bs != nullptr;
-  const int tile = variant ? variant : pick_tile(layout, tiles64, splitk, planes);
+  const int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
   const bool tn_big = layout == SCA_GEMM_TN && tile >= kTnFirst && tile <= kTnLast && tn_ok(a, nprob);
-  const bool x6 = tile >= 50 && x6_ok(a, nprob, (tile == 50 || tile == 55 || tile == 56 || tile >= 60) ? 16 : 32);
-  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big || x6) && glds_ok(a, nprob) &&
+  if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&
       vec_ok(a, nprob, layout)) {
     a.counters = counters;
     do_reduce = false;
@@ -3089,36 +1939,6 @@ extern "C" long sca_gemm_splitk_counters(int nprob, int maxM, int maxN) {
 extern "C" int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_problem* probs, int splitk,
                                      float* workspace, unsigned* counters, void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, true, true, counters);
-}
-
-extern "C" int sca_split3(int nprob, const sca_split_problem* probs, void* stream) {
-  if (nprob <= 0) return SCA_OK;
-  if (nprob > SCA_SPLIT_MAX_PROBLEMS || !probs) {
-    sca_set_error("sca_split3: bad nprob");
-    return SCA_ERR_ARG;
-  }
-  SplitArgs a;
-  long maxn = 0;
-  for (int i = 0; i < nprob; ++i) {
-    const sca_split_problem& P = probs[i];
-    if (P.n < 0 || P.plane < P.n || (P.n > 0 && (!P.src || !P.dst)) || (reinterpret_cast<uintptr_t>(P.src) & 15) ||
-        (reinterpret_cast<uintptr_t>(P.dst) & 7) || (P.plane & 3)) {
-      sca_set_error("sca_split3: bad problem (src 16-B / dst 8-B aligned, plane >= n and a multiple of 4)");
-      return SCA_ERR_ARG;
-    }
-    a.p[i] = P;
-    maxn = maxn > P.n ? maxn : P.n;
-  }
-  if (maxn == 0) return SCA_OK;
-  long blocks = (maxn / 4 + 255) / 256;
-  if (blocks < 1) blocks = 1;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
-  if (hipGetLastError() != hipSuccess) {
-    sca_set_error("sca_split3: launch failed");
-    return SCA_ERR_LAUNCH;
-  }
-  return SCA_OK;
 }
 
 extern "C" int sca_gemm_variant(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
@@ -3196,26 +2016,8 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
     maxM = maxM > P.M ? maxM : P.M;
   }
   if (maxM == 0) return SCA_OK;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // x6 form: every B operand given as planes
-  bool x6 = N == LG_BN;
-  auto planes_ok = [](const unsigned short* Bs, long plane, int ldb) {
-    return Bs && !(reinterpret_cast<uintptr_t>(Bs) & 15) && !(plane & 7) && !(ldb & 7);
-  };
-  for (int i = 0; i < nprob && x6; ++i) {
-    const sca_gemm_seg& S = probs[i].seg[0];
-    x6 = planes_ok(S.Bs, S.bs_plane, S.ldb) && S.K % 16 == 0;
-    for (int q = 0; q < ln[i].npass && x6; ++q) x6 = planes_ok(ln[i].pass[q].Bs, ln[i].pass[q].bs_plane, ln[i].pass[q].ldb);
-  }
-  if (x6) {
-    if (chain)
-      hipLaunchKernelGGL((gemm_ln_x6_kernel<true>), dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((gemm_ln_x6_kernel<false>), dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
-    if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
-    return SCA_OK;
-  }
   const int bm = sca_gemm_ln_rows(nprob, maxM, chain);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (N != LG_BN) {
     hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 2>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   } else if (chain) {
@@ -3279,23 +2081,6 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
   }
   if (maxM == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  bool x6 = N == LG_BN;  // x6 form: every B operand given as planes
-  for (int i = 0; i < nprob && x6; ++i) {
-    const sca_gemm_lnb_problem& L = lnb[i];
-    for (int s = 0; s < probs[i].nseg && x6; ++s) {
-      const sca_gemm_seg& S = probs[i].seg[s];
-      x6 = S.Bs && !(reinterpret_cast<uintptr_t>(S.Bs) & 15) && !(S.bs_plane & 7) && !(S.ldb & 7) && S.K % 16 == 0;
-    }
-    if (L.wo) {
-      const long ldw = L.ldw ? L.ldw : (long)LG_BN * (L.npass ? L.npass : 1);
-      x6 = x6 && L.wo_s && !(reinterpret_cast<uintptr_t>(L.wo_s) & 15) && !(L.wo_plane & 7) && !(ldw & 7);
-    }
-  }
-  if (x6) {
-    hipLaunchKernelGGL(gemm_lnb_x6_kernel, dim3((maxM + 31) / 32, 1, nprob), dim3(256), 0, st, a);
-    if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }
-    return SCA_OK;
-  }
   if (N == LG_BN) hipLaunchKernelGGL(gemm_lnb_kernel<1>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   else hipLaunchKernelGGL(gemm_lnb_kernel<2>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }

@@ -4,7 +4,6 @@ MSCA_Net (body_encoder, left_encoder, right_encoder, coordinates_fusion) so the 
 subset of a reference checkpoint loads into it.  BASELINE config 3 ("full encoder")."""
 from torch import nn
 
-from . import ops
 from .fusion import CoordinatesFusion
 from .keypoint_module import KeypointModule, joint_index_tensors, keypoint_streams_forward
 
@@ -27,7 +26,6 @@ class SCAEncoder(nn.Module):
         idx = getattr(self, "_idx", None)
         if idx is None or idx[0].device != keypoints.device:
             idx = self._idx = joint_index_tensors(mods, keypoints.device)
-        with ops.weight_planes(ops.linear_weights([self])):
-            body, left, right = keypoint_streams_forward(mods, idx, keypoints, mask, with_residual=True)
-            fuse = self.coordinates_fusion(left, right, body)
+        body, left, right = keypoint_streams_forward(mods, idx, keypoints, mask, with_residual=True)
+        fuse = self.coordinates_fusion(left, right, body)
         return fuse, left, right, body

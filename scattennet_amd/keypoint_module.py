@@ -235,11 +235,9 @@ def joint_index_tensors(mods, device):
 
 
 def keypoint_streams_forward(mods, joint_idx, keypoints, attention_mask, with_residual=True):
-    """G KeypointModules in lock-step over one (B, T, K_all, 2) tensor (stream slicing fused).
-    Every Linear weight of the streams is split for the x6 GEMMs in one launch up front."""
-    with ops.weight_planes(ops.linear_weights(mods)):
-        xe, ye = coordinate_mapping_grouped([m.coordinate_mapping for m in mods], keypoints, joint_idx)
-        out, _ = sca_grouped([m.sca for m in mods], xe, ye, attention_mask)
-        if with_residual:
-            out = residual_network_grouped([m.residual for m in mods], out)
+    """G KeypointModules in lock-step over one (B, T, K_all, 2) tensor (stream slicing fused)."""
+    xe, ye = coordinate_mapping_grouped([m.coordinate_mapping for m in mods], keypoints, joint_idx)
+    out, _ = sca_grouped([m.sca for m in mods], xe, ye, attention_mask)
+    if with_residual:
+        out = residual_network_grouped([m.residual for m in mods], out)
     return out

@@ -70,22 +70,18 @@ class _timed:
 
 
 # name prefixes of every kernel that can run a layout's plain GEMM (tests count launches by them)
-GEMM_KERNELS = {lay: (f"gemm_glds_kernel<{lay},", f"gemm_x6d_kernel<{lay},", f"gemm_x6_kernel<{lay},",
-                      f"gemm_kernel<{lay}") for lay in range(3)}
+GEMM_KERNELS = {lay: (f"gemm_glds_kernel<{lay},", f"gemm_kernel<{lay}") for lay in range(3)}
 
 # rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>:
 # the ring depth pick_tile chooses, 3 stages forward, 2 for the gradient layouts)
 _GEMM_NAMES = {0: "gemm_glds_kernel<0, 3>", 1: "gemm_glds_kernel<1, 2>", 2: "gemm_glds_kernel<2, 2>"}
 
 # --------------------------------------------------------------------------- launch helpers
-_NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0, None, 0)
+_NOSEG = L.GemmSeg(None, None, 0, 0, 0, 0.0)
 
 
-def _seg(A, B, lda, ldb, K, alpha=1.0, Bs=None):
-    """Bs: B's three bf16 pieces (planes_of(B) / split3), read by the x6 kernels instead of B."""
-    if Bs is None:
-        return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha, None, 0)
-    return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha, Bs.ptr_for(B), Bs.plane)
+def _seg(A, B, lda, ldb, K, alpha=1.0):
+    return L.GemmSeg(A.data_ptr(), B.data_ptr(), lda, ldb, K, alpha)
 
 
 def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=0, aux=None, ldx=0,
@@ -98,128 +94,6 @@ def _prob(segs, C, M, N, ldc, bias=None, post_scale=1.0, resid=None, ldr=0, epi=
     return L.GemmProblem((L.GemmSeg * 3)(*s), len(segs), M, N, C.data_ptr(), ldc, epi, ptr(bias), post_scale,
                          ptr(resid), ldr, ptr(aux), ldx, ptr(aux_out), ldo, ptr(bias_grad), bias_grad_scale,
                          seed, p)
-
-
-# --------------------------------------------------------------------------- x6 operand planes
-class Planes:
-    """The three bf16 pieces of an fp32 tensor (sca_split3; include/scatten.h): `t` holds
-    [3][plane] 16-bit values, piece p of element i at t[p * plane + i].  A GEMM segment whose B
-    operand is (a row block of) the source tensor reads them instead of splitting B itself."""
-    __slots__ = ("t", "base_ptr", "plane", "numel")
-
-    def __init__(self, src):
-        self.numel = src.numel()
-        self.plane = -(-self.numel // 8) * 8
-        self.t = torch.empty(3 * self.plane, dtype=torch.int16, device=src.device)
-        self.base_ptr = src.data_ptr()
-
-    def ptr_for(self, B):
-        """Address of B's first element in plane 0 (B a view into the split tensor)."""
-        off = B.data_ptr() - self.base_ptr
-        if off < 0 or off >= 4 * self.numel:
-            raise ValueError("Planes.ptr_for: tensor is not a view of the split source")
-        return self.t.data_ptr() + off // 2
-
-
-# fp32 products on the bf16 matrix cores (csrc/x6.h): the Linear weights are split once per
-# forward pass and the NT / NN GEMMs that read them run the x6 LDS-DMA kernel.  False: every
-# GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32) — the same results to fp32 rounding.
-X6 = True
-# which launch families take the planes (tools/gemm_ln_bench.py, bench.py --x6): the plain
-# NT / NN GEMMs, the GEMM + LayerNorm forward, its backward
-X6_KINDS = {"gemm": True, "ln": False, "lnb": False}
-_PLANES = None  # id(weight) -> Planes inside a weight_planes scope
-
-
-def set_x6(kinds):
-    """kinds: iterable of "gemm" / "ln" / "lnb" (the others run the fp32 kernels)."""
-    kinds = set(kinds)
-    for k in X6_KINDS:
-        X6_KINDS[k] = k in kinds
-
-
-def _strip_planes(probs, lns=None, lnbs=None):
-    for p in probs:
-        for j in range(p.nseg):
-            p.seg[j].Bs, p.seg[j].bs_plane = None, 0
-    for ln in lns or ():
-        for q in range(ln.npass):
-            ln.passes[q].Bs, ln.passes[q].bs_plane = None, 0
-    for o in lnbs or ():
-        o.wo_s, o.wo_plane = None, 0
-
-
-class weight_planes:
-    """One forward pass's weight planes: the 2-D fp32 weights in `weights` are split in one
-    sca_split3 launch (per 64) on entry, and every GEMM reading one of them uses its planes —
-    in the forward, and in the backward through the references the Functions keep.  Under
-    graph capture the split launch is part of the step, so replays see the current weights.
-    A nested scope reuses the outer one."""
-
-    def __init__(self, weights):
-        self.weights = weights
-
-    def __enter__(self):
-        global _PLANES
-        self.prev = _PLANES
-        if X6 and _PLANES is None and not _LIBRARY_MODE:
-            seen, ws = set(), []
-            for w in self.weights:
-                if (w is not None and w.dim() == 2 and w.is_cuda and w.dtype == torch.float32 and
-                        w.is_contiguous() and id(w) not in seen):
-                    seen.add(id(w))
-                    ws.append(w)
-            _PLANES = dict(zip(map(id, ws), split3(ws))) if ws else {}
-        return self
-
-    def __exit__(self, *exc):
-        global _PLANES
-        _PLANES = self.prev
-
-
-def linear_weights(mods):
-    """The nn.Linear weights under the modules `mods` (what the x6 GEMMs read as B)."""
-    return [m.weight for mod in mods for m in mod.modules() if isinstance(m, torch.nn.Linear)]
-
-
-def wplanes(Ws):
-    """id(W) -> Planes for the weights Ws (x6 on): from the enclosing weight_planes scope,
-    the missing ones split now in one launch.  Empty when x6 is off."""
-    if not X6 or _LIBRARY_MODE:
-        return {}
-    out, miss = {}, []
-    for w in Ws:
-        p = _PLANES.get(id(w)) if _PLANES is not None else None
-        if p is not None and p.base_ptr == w.data_ptr():
-            out[id(w)] = p
-        elif w.is_contiguous() and id(w) not in out:
-            miss.append(w)
-    if miss:
-        uniq = list({id(w): w for w in miss}.values())
-        for w, p in zip(uniq, split3(uniq)):
-            out[id(w)] = p
-            if _PLANES is not None:
-                _PLANES[id(w)] = p
-    return out
-
-
-def _wseg(A, W, lda, ldb, K, pl, alpha=1.0):
-    """A GEMM segment whose B operand is the weight W (its planes from `pl` when present)."""
-    return _seg(A, W, lda, ldb, K, alpha, Bs=pl.get(id(W)) if pl else None)
-
-
-def split3(srcs):
-    """Planes of each contiguous fp32 tensor in `srcs`, one sca_split3 launch per 64."""
-    out = [Planes(s) for s in srcs]
-    lib = L.lib()
-    st = L.stream_handle()
-    for c in range(0, len(srcs), L.SPLIT_MAX_PROBLEMS):
-        chunk = list(zip(srcs[c:c + L.SPLIT_MAX_PROBLEMS], out[c:c + L.SPLIT_MAX_PROBLEMS]))
-        arr = (L.SplitProblem * len(chunk))(*[L.SplitProblem(s.data_ptr(), p.t.data_ptr(), p.numel, p.plane)
-                                              for s, p in chunk])
-        with _timed("split3_kernel", 0.0):
-            L.check(lib.sca_split3(len(chunk), arr, st), "sca_split3")
-    return out
 
 
 # --------------------------------------------------------------------------- dropout
@@ -322,33 +196,16 @@ def _splitk_counters(n, device=None):
 _TILE_NAMES = {36: "gemm_tnk_kernel<3, 1>", 37: "gemm_tnk_kernel<4, 1>"}
 
 
-def _kernel_name(layout, chunk, tile):
-    """The kernel a grouped launch runs, as rocprofv3 names it (mirrors pick_tile / launch_tile:
-    NT / NN with every B pre-split -> the x6 LDS-DMA kernel)."""
-    if tile:
-        return _TILE_NAMES.get(tile, f"gemm tile {tile}")
-    planes = layout != L.GEMM_TN and all(p.seg[j].Bs for p in chunk for j in range(p.nseg))
-    ok = all(p.seg[j].K % 16 == 0 for p in chunk for j in range(p.nseg)) and all(
-        p.M % 4 == 0 and p.N % (128 if layout == L.GEMM_NN else 4) == 0 for p in chunk)
-    if planes and ok:
-        tiles64 = sum(-(-p.M // 64) * -(-p.N // 64) for p in chunk)
-        return f"gemm_x6d_kernel<{layout}, 128, 128, 3>" if tiles64 // 4 >= 256 else \
-            f"gemm_x6d_kernel<{layout}, 64, 128, 3>"
-    return _GEMM_NAMES[layout]
-
-
 def gemm(layout, probs, splitk=1, ws=None, tile=0):
     """tile: a kernel variant for this call only (sca_gemm_variant ids; 0 = the heuristic),
     passed per call through the C ABI (no process-global override is touched)."""
     lib = L.lib()
+    kname = _TILE_NAMES.get(tile, f"gemm tile {tile}") if tile else _GEMM_NAMES[layout]
     st = L.stream_handle()
     for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
-        if not X6_KINDS["gemm"]:
-            _strip_planes(arr)
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
-        kname = _kernel_name(layout, list(arr), tile) if _PROFILER else ""
         if splitk > 1 and _SPLITK_FUSED and "sca_gemm_splitk_fused" not in L.MISSING:
             cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
                                                                 max(p.N for p in chunk)),
@@ -402,20 +259,13 @@ def gemm_ln(probs, lns, eps):
         chunk, lchunk = probs[i:i + L.GEMM_LN_MAX_PROBLEMS], lns[i:i + L.GEMM_LN_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
         larr = (L.GemmLnProblem * len(lchunk))(*lchunk)
-        if not X6_KINDS["ln"]:
-            _strip_planes(arr, larr)
-            chunk, lchunk = list(arr), list(larr)
         flops = sum(2.0 * p.M * p.N * (p.seg[0].K + 256 * ln.npass) for p, ln in zip(chunk, lchunk)) \
             if _PROFILER else 0.0
         # the variant sca_gemm_ln picks, for the kernel name rocprofv3 shows
         chain = any(ln.npass > 0 for ln in lchunk)
         nc = chunk[0].N // 256
         bm = 32 if nc > 1 else lib.sca_gemm_ln_rows(len(chunk), max(p.M for p in chunk), int(chain))
-        x6 = nc == 1 and all(p.seg[0].Bs for p in chunk) and all(ln.passes[q].Bs for ln in lchunk
-                                                                   for q in range(ln.npass))
-        kname = (f"gemm_ln_x6_kernel<{'true' if chain else 'false'}>" if x6 else
-                 f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}>")
-        with _timed(kname, flops):
+        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}>", flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
@@ -507,19 +357,15 @@ class NextProjections:
     def passes(self, g, M, like):
         """Producer: the ChainPass list of stream g (outputs allocated here)."""
         ps, outs = [], []
-        pl = wplanes([W for W, _, _, _ in self.specs[g]])
         for W, b, scale, gelu in self.specs[g]:
             n = W.shape[0]
             C = like.new_empty(M, n)
             A = like.new_empty(M, n) if gelu else None
-            wp = pl.get(id(W))
             for p in range(n // 256):
                 ps.append(L.ChainPass(W[256 * p:].data_ptr(), W.stride(0),
                                       b[256 * p:].data_ptr() if b is not None else None, float(scale),
                                       L.EPI_GELU if gelu else 0, C[:, 256 * p:].data_ptr(), n,
-                                      A[:, 256 * p:].data_ptr() if gelu else None, n if gelu else 0,
-                                      wp.ptr_for(W[256 * p:]) if wp is not None else None,
-                                      wp.plane if wp is not None else 0))
+                                      A[:, 256 * p:].data_ptr() if gelu else None, n if gelu else 0))
             outs.append((C, A))
         self.outs[g] = outs
         return ps
@@ -581,25 +427,16 @@ def gemm_lnb(probs, lnp):
     n2 = lnp[0].wo.shape[1] if chain else 0
     dout = [o.v.new_empty(*o.v.shape[:-1], n2) for o in lnp] if chain else [None] * len(lnp)
     arr = (L.GemmProblem * len(probs))(*probs)
-    wpl = wplanes([o.wo for o in lnp]) if chain else {}
-
-    def wo_planes(o):
-        p = wpl.get(id(o.wo))
-        return (p.ptr_for(o.wo), p.plane) if p is not None else (None, 0)
     larr = (L.GemmLnbProblem * len(lnp))(*[L.GemmLnbProblem(o.v.data_ptr(), o.mean.data_ptr(), o.rstd.data_ptr(),
                                                            o.gamma.data_ptr(), dv[g].data_ptr(), part[g].data_ptr(),
                                                            ptr(o.wo) if chain else None, ptr(dout[g]),
                                                            ptr(o.aux) if chain else None, n2 // 256, n2,
-                                                           ptr(o.tab), o.T, *wo_planes(o))
+                                                           ptr(o.tab), o.T)
                                             for g, o in enumerate(lnp)])
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
-    if not X6_KINDS["lnb"]:
-        _strip_planes(arr, lnbs=larr)
-    x6 = probs[0].N == 256 and all(p.seg[j].Bs for p in arr for j in range(p.nseg)) and (
-        not chain or all(o.wo_s for o in larr))
-    with _timed("gemm_lnb_x6_kernel" if x6 else f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
+    with _timed(f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
 
@@ -1175,7 +1012,6 @@ class AttentionBlock(Function):
         W = ts[o_:o_ + 6 * G]
         Wo, bo = ts[o_ + 6 * G:o_ + 7 * G], ts[o_ + 7 * G:o_ + 8 * G]
         L.require_device(*xq, *xkv)
-        pl = wplanes([W[6 * g + j] for g in range(G) for j in (0, 2, 4)] + list(Wo))
         B, T, d = xq[0].shape
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
@@ -1198,9 +1034,9 @@ class AttentionBlock(Function):
                 q.append(xq[g].new_empty(B, T, d))
                 k.append(xq[g].new_empty(B, Tk, d))
                 v.append(xq[g].new_empty(B, Tk, d))
-                probs.append(_prob([_wseg(xf, Wq, d, d, d, pl)], q[g], B * T, d, d, bias=bq, post_scale=scale))
-                probs.append(_prob([_wseg(kf, Wk, d, d, d, pl)], k[g], B * Tk, d, d, bias=bk))
-                probs.append(_prob([_wseg(kf, Wv, d, d, d, pl, av)], v[g], B * Tk, d, d, bias=bv))
+                probs.append(_prob([_seg(xf, Wq, d, d, d)], q[g], B * T, d, d, bias=bq, post_scale=scale))
+                probs.append(_prob([_seg(kf, Wk, d, d, d)], k[g], B * Tk, d, d, bias=bk))
+                probs.append(_prob([_seg(kf, Wv, d, d, d, av)], v[g], B * Tk, d, d, bias=bv))
             gemm(L.GEMM_NT, probs)
         # attention-probability dropout (attention.py:67-69): its seeds precede the block's own
         attn_drop = (attn_p, dropout_seeds(G)) if attn_p > 0 else None
@@ -1212,7 +1048,7 @@ class AttentionBlock(Function):
             vs, ys, means, rstds = _ln_fwd_outputs(xq)
         else:
             ys = vs = [torch.empty_like(x) for x in xq]
-        probs = [_prob([_wseg(_flat(o[g]), Wo[g], d, d, d, pl)], vs[g], B * T, d, d, bias=bo[g],
+        probs = [_prob([_seg(_flat(o[g]), Wo[g], d, d, d)], vs[g], B * T, d, d, bias=bo[g],
                        resid=_flat(xq[g]) if has_resid else None, ldr=d,
                        drop=(seeds[g], drop_p) if drop_p > 0 else None) for g in range(G)]
         if ln:
@@ -1223,7 +1059,6 @@ class AttentionBlock(Function):
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = G, kind, H, scale, plus_one, has_resid
         ctx.attn_drop = attn_drop
-        ctx.pl = pl
         ctx.drop_p, ctx.seeds, ctx.ln = drop_p, seeds, ln
         ctx.bet = tuple(bet) if ln else ()  # parameters (leaves): identify their gradients' slots
         ctx.lnsaved = _attach_ln_saved(ys, vs, means, rstds, gam, Wo if drop_p == 0 else None) if ln else None
@@ -1251,7 +1086,6 @@ class AttentionBlock(Function):
         B, T, d = xq[0].shape
         Tk = xkv[0].shape[1]
         av = 0.5 if cross else 1.0
-        pl = getattr(ctx, "pl", None)
         dgam = dbet = ()
         ln_finish = None
         do = None
@@ -1269,7 +1103,7 @@ class AttentionBlock(Function):
         # out-projection: dO = dY' Wo (unless the consumer's sca_gemm_lnb already chained it)
         if do is None:
             do = [torch.empty_like(t) for t in o]
-            gemm(L.GEMM_NN, [_prob([_wseg(_flat(dyo[g]), Wo[g], d, d, d, pl)], do[g], B * T, d, d) for g in range(G)])
+            gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), Wo[g], d, d, d)], do[g], B * T, d, d) for g in range(G)])
         # dq comes back pre-multiplied by the q scale and dv by alpha_v, so that every GEMM below
         # runs with unit segment scales: dX = dq' Wq + dk Wk + dv' Wv, dWq = dq'^T x, ...
         dq, dk, dv = _attn_bwd(G, H, kind == "causal", ctx.plus_one, key_valid, add_mask, q, k, v, o, sm, sl, do,
@@ -1284,12 +1118,11 @@ class AttentionBlock(Function):
             gx = torch.empty_like(xq[g])
             if cross:
                 gkv = torch.empty_like(xkv[g])
-                probs.append(_prob([_wseg(dqf, Wq, d, d, d, pl)], gx, B * T, d, d, resid=r, ldr=d))
-                kvprobs.append(_prob([_wseg(dkf, Wk, d, d, d, pl), _wseg(dvf, Wv, d, d, d, pl)], gkv, B * Tk, d, d))
+                probs.append(_prob([_seg(dqf, Wq, d, d, d)], gx, B * T, d, d, resid=r, ldr=d))
+                kvprobs.append(_prob([_seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)], gkv, B * Tk, d, d))
                 dxkv.append(gkv)
             else:
-                probs.append(_prob([_wseg(dqf, Wq, d, d, d, pl), _wseg(dkf, Wk, d, d, d, pl),
-                                    _wseg(dvf, Wv, d, d, d, pl)],
+                probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
                                    gx, B * T, d, d, resid=r, ldr=d))
             dxq.append(gx)
         if ctx.lnprev is not None:
@@ -1328,18 +1161,17 @@ class LinearResidual(Function):
         W, b = ts[G:2 * G], ts[2 * G:3 * G]
         r = _contig(ts[3 * G:4 * G]) if has_r else [None] * G
         L.require_device(*x)
-        pl = wplanes(W)
         probs, ys = [], []
         for g in range(G):
             n_out, n_in = W[g].shape
             lead = x[g].shape[:-1]
             M = x[g].numel() // n_in
             y = x[g].new_empty(*lead, n_out)
-            probs.append(_prob([_wseg(_flat(x[g]), W[g], n_in, n_in, n_in, pl)], y, M, n_out, n_out, bias=b[g],
+            probs.append(_prob([_seg(_flat(x[g]), W[g], n_in, n_in, n_in)], y, M, n_out, n_out, bias=b[g],
                                resid=r[g], ldr=n_out))
             ys.append(y)
         gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.has_r, ctx.b, ctx.pl = G, has_r, tuple(b), pl  # biases: parameters (leaves) or None
+        ctx.G, ctx.has_r, ctx.b = G, has_r, tuple(b)  # biases: parameters (leaves) or None
         ctx.save_for_backward(*x, *W)
         return tuple(ys)
 
@@ -1354,8 +1186,7 @@ class LinearResidual(Function):
             n_out, n_in = W[g].shape
             M = x[g].numel() // n_in
             dx = torch.empty_like(x[g])
-            probs.append(_prob([_wseg(_flat(dys[g]), W[g], n_out, n_in, n_out, getattr(ctx, "pl", None))], dx, M,
-                               n_in, n_in))
+            probs.append(_prob([_seg(_flat(dys[g]), W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
             dxs.append(dx)
         gemm(L.GEMM_NN, probs)
         wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
@@ -1378,7 +1209,6 @@ class FeedForwardResidual(Function):
         if ln:
             gam, bet = ts[5 * G:6 * G], ts[6 * G:7 * G]
         L.require_device(*x)
-        pl = wplanes(list(W1) + list(W2))
         B, T, d = x[0].shape
         M = B * T
         F_ = W1[0].shape[0]
@@ -1397,14 +1227,14 @@ class FeedForwardResidual(Function):
         else:
             zs = [x[0].new_empty(M, F_) for _ in range(G)]
             acts = [x[0].new_empty(M, F_) for _ in range(G)]
-            gemm(L.GEMM_NT, [_prob([_wseg(_flat(x[g]), W1[g], d, d, d, pl)], acts[g], M, F_, F_, bias=b1[g],
+            gemm(L.GEMM_NT, [_prob([_seg(_flat(x[g]), W1[g], d, d, d)], acts[g], M, F_, F_, bias=b1[g],
                                    epi=L.EPI_GELU, aux_out=zs[g], ldo=F_,
                                    drop=(s1[g], drop_p) if drop_p > 0 else None) for g in range(G)])
         if ln:
             vs, ys, means, rstds = _ln_fwd_outputs(x)
         else:
             ys = vs = [torch.empty_like(x[g]) for g in range(G)]
-        probs = [_prob([_wseg(acts[g], W2[g], F_, F_, F_, pl)], vs[g], M, d, d, bias=b2[g],
+        probs = [_prob([_seg(acts[g], W2[g], F_, F_, F_)], vs[g], M, d, d, bias=b2[g],
                        resid=_flat(x[g]) if has_r else None, ldr=d,
                        drop=(s2[g], drop_p) if drop_p > 0 else None) for g in range(G)]
         if ln:
@@ -1414,7 +1244,6 @@ class FeedForwardResidual(Function):
         else:
             gemm(L.GEMM_NT, probs)
         ctx.G, ctx.has_r, ctx.drop_p, ctx.s1, ctx.s2, ctx.ln = G, has_r, drop_p, s1, s2, ln
-        ctx.pl = pl
         ctx.b1, ctx.b2, ctx.bet = tuple(b1), tuple(b2), (tuple(bet) if ln else ())  # parameters (leaves)
         # dz = (dL/dv W2) * gelu'(z) chained into the consumer's launch (no dropout in between)
         dz_chain = drop_p == 0 and _CHAIN_DZ
@@ -1429,7 +1258,6 @@ class FeedForwardResidual(Function):
         G = ctx.G
         sv = ctx.saved_tensors
         x, W1, W2, zs, acts = (sv[i * G:(i + 1) * G] for i in range(5))
-        pl = getattr(ctx, "pl", None)
         dgam = dbet = ()
         ln_finish = dzc = None
         if ctx.ln:  # through the fused LayerNorm first: dys becomes the gradient of v
@@ -1451,12 +1279,12 @@ class FeedForwardResidual(Function):
             dz = [t.reshape(M, F_) for t in dzc]
         else:
             dz = [x[0].new_empty(M, F_) for _ in range(G)]
-            gemm(L.GEMM_NN, [_prob([_wseg(_flat(dyo[g]), W2[g], d, F_, d, pl)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
+            gemm(L.GEMM_NN, [_prob([_seg(_flat(dyo[g]), W2[g], d, F_, d)], dz[g], M, F_, F_, epi=L.EPI_DGELU,
                                    aux=zs[g], ldx=F_, drop=(ctx.s1[g], p) if p > 0 else None) for g in range(G)])
         # dx = dz W1 + dy   (residual); with `lnprev` the input's LayerNorm backward rides in
         # the same launch (sca_gemm_lnb)
         dx = [torch.empty_like(x[g]) for g in range(G)]
-        probs = [_prob([_wseg(dz[g], W1[g], F_, d, F_, pl)], dx[g], M, d, d,
+        probs = [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
                        resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)]
         if ctx.lnprev is not None:
             hand_off(ctx.lnprev, dx, *gemm_lnb(probs, ctx.lnprev))
@@ -1702,19 +1530,18 @@ class LinearGelu(Function):
         W, b = ts[G:2 * G], ts[2 * G:3 * G]
         r = _contig(ts[3 * G:4 * G]) if has_r else [None] * G
         L.require_device(*x)
-        pl = wplanes(W)
         probs, ys, zs = [], [], []
         for g in range(G):
             n_out, n_in = W[g].shape
             M = x[g].numel() // n_in
             y = x[g].new_empty(*x[g].shape[:-1], n_out)
             z = x[g].new_empty(M, n_out)
-            probs.append(_prob([_wseg(_flat(x[g]), W[g], n_in, n_in, n_in, pl)], y, M, n_out, n_out, bias=b[g],
+            probs.append(_prob([_seg(_flat(x[g]), W[g], n_in, n_in, n_in)], y, M, n_out, n_out, bias=b[g],
                                resid=r[g], ldr=n_out, epi=L.EPI_GELU, aux_out=z, ldo=n_out))
             ys.append(y)
             zs.append(z)
         gemm(L.GEMM_NT, probs)
-        ctx.G, ctx.has_r, ctx.b, ctx.pl = G, has_r, tuple(b), pl  # biases: parameters (leaves) or None
+        ctx.G, ctx.has_r, ctx.b = G, has_r, tuple(b)  # biases: parameters (leaves) or None
         ctx.save_for_backward(*x, *W, *zs)
         return tuple(ys)
 
@@ -1730,8 +1557,7 @@ class LinearGelu(Function):
             n_out, n_in = W[g].shape
             M = x[g].numel() // n_in
             dx = torch.empty_like(x[g])
-            probs.append(_prob([_wseg(dz[g], W[g], n_out, n_in, n_out, getattr(ctx, "pl", None))], dx, M, n_in,
-                               n_in))
+            probs.append(_prob([_seg(dz[g], W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
             dxs.append(dx)
         gemm(L.GEMM_NN, probs)
         wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])

@@ -13,9 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4", 36: "TNK3",
-         50: "x6_128sq16", 51: "x6_128x64", 52: "x6_64x128", 53: "x6_64sq", 54: "x6_128sq32", 55: "x6_128x64k16",
-         56: "x6_64sq16", 60: "x6d128s3", 61: "x6d128s4", 62: "x6d64s3", 63: "x6d64s4"}
+TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4"}
 
 
 def make_case(name, layout, shapes, splitk=1, segs=1):
@@ -29,15 +27,11 @@ def make_case(name, layout, shapes, splitk=1, segs=1):
         for _ in range(segs):
             if layout == L.GEMM_NT:
                 A, B = torch.randn(M, K, device=dev), torch.randn(N, K, device=dev)
-                Bs = ops.split3([B])[0]  # pre-split weights (x6 LDS-DMA variants 60-63)
-                seglist.append(ops._seg(A, B, K, K, K, Bs=Bs))
-                keep.append(Bs)
+                seglist.append(ops._seg(A, B, K, K, K))
                 ref += A.double().cpu() @ B.double().cpu().T
             elif layout == L.GEMM_NN:
                 A, B = torch.randn(M, K, device=dev), torch.randn(K, N, device=dev)
-                Bs = ops.split3([B])[0]
-                seglist.append(ops._seg(A, B, K, N, K, Bs=Bs))
-                keep.append(Bs)
+                seglist.append(ops._seg(A, B, K, N, K))
                 ref += A.double().cpu() @ B.double().cpu()
             else:
                 A, B = torch.randn(K, M, device=dev), torch.randn(K, N, device=dev)
@@ -102,26 +96,18 @@ def main():
                 del TILES[k]
     lib = L.lib()
     for c in cases:
-        if c["layout"] != L.GEMM_TN:
-            TL = [t for t in TILES if t != 36]
-        else:  # no pre-split B: the LDS-DMA x6 variants (60+) are NT / NN only
-            TL = [t for t in TILES if t < 60]
-        c["tiles"] = TL
-        for t in TL:
+        for t in TILES:
             lib.sca_gemm_tile_override(c["layout"], t)
             ops.gemm(c["layout"], c["probs"], c["splitk"], c["ws"])
             torch.cuda.synchronize()
-            worst = 0.0
             for C, ref in ([] if args.no_check else c["refs"]):
                 err = float((C.double().cpu() - ref).abs().max() / ref.abs().max())
-                worst = max(worst, err)
                 assert err < 1e-5, (c["name"], TILES[t], err)
-            c.setdefault("err", {})[t] = worst
     print(f"{'case':34s} " + " ".join(f"{v:>9s}" for v in TILES.values()) + "   (TFLOP/s)")
     res = {}
     graphs = {}
     for c in cases:  # capture `iters` launches per (case, tile): times the GPU, not the Python launcher
-        for t in c["tiles"]:
+        for t in TILES:
             lib.sca_gemm_tile_override(c["layout"], t)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -130,7 +116,7 @@ def main():
             graphs[(c["name"], t)] = g
     for rnd in range(args.rounds):
         for c in cases:
-            for t in c["tiles"]:
+            for t in TILES:
                 g = graphs[(c["name"], t)]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -140,13 +126,7 @@ def main():
                 tf = c["flops"] * args.iters / (e0.elapsed_time(e1) / 1e3) / 1e12
                 res.setdefault((c["name"], t), []).append(tf)
     for c in cases:
-        print(f"{c['name']:34s} " + " ".join(f"{max(res[(c['name'], t)]):9.1f}" if (c['name'], t) in res
-                                             else f"{'-':>9s}" for t in TILES))
-    if not args.no_check:
-        print("max |C - C_fp64| / max |C_fp64| per variant:")
-        for c in cases:
-            print(f"{c['name']:34s} " + " ".join(f"{c['err'][t]:9.1e}" if t in c["err"] else f"{'-':>9s}"
-                                                 for t in TILES))
+        print(f"{c['name']:34s} " + " ".join(f"{max(res[(c['name'], t)]):9.1f}" for t in TILES))
     for lay in range(3):
         lib.sca_gemm_tile_override(lay, 0)
 

@@ -28,17 +28,11 @@ def case(G, M, K, N=256):
     rstd = [torch.empty(M, device=dev) for _ in range(G)]
     probs = [ops._prob([ops._seg(A[g], W[g], K, K, K)], v[g], M, N, N, bias=b[g], resid=r[g], ldr=N)
              for g in range(G)]
-    Wp = ops.split3(W)  # x6: the weights' bf16 planes
-    probs6 = [ops._prob([ops._seg(A[g], W[g], K, K, K, Bs=Wp[g])], v[g], M, N, N, bias=b[g], resid=r[g], ldr=N)
-              for g in range(G)]
     lns = [L.GemmLnProblem(gam[g].data_ptr(), bet[g].data_ptr(), y[g].data_ptr(), mean[g].data_ptr(),
                            rstd[g].data_ptr()) for g in range(G)]
 
     def fused():
         ops.gemm_ln(probs, lns, 1e-5)
-
-    def fused6():
-        ops.gemm_ln(probs6, lns, 1e-5)
 
     def split():
         ops.gemm(L.GEMM_NT, probs)
@@ -56,24 +50,16 @@ def case(G, M, K, N=256):
     nxt = ops.NextProjections([[(W1[g], b1[g], 1.0, True)] for g in range(G)])
 
     def chained():
-        x6, ops.X6 = ops.X6, False
-        try:
-            ops.gemm_ln(probs, ops._chain_lns(nxt, G, M, v[0], gam, bet, y, mean, rstd), 1e-5)
-        finally:
-            ops.X6 = x6
-
-    def chained6():  # (inside a weight_planes scope: the passes' planes come from it)
-        ops.gemm_ln(probs6, ops._chain_lns(nxt, G, M, v[0], gam, bet, y, mean, rstd), 1e-5)
+        ops.gemm_ln(probs, ops._chain_lns(nxt, G, M, v[0], gam, bet, y, mean, rstd), 1e-5)
 
     def unchained():
         ops.gemm_ln(probs, lns, 1e-5)
         ops.gemm(L.GEMM_NT, [ops._prob([ops._seg(y[g], W1[g], N, N, N)], act[g], M, 768, 768, bias=b1[g],
                                        epi=L.EPI_GELU, aux_out=z[g], ldo=768) for g in range(G)])
 
-    keep = (A, W, b, r, gam, bet, v, y, mean, rstd, W1, b1, z, act, Wp)
+    keep = (A, W, b, r, gam, bet, v, y, mean, rstd, W1, b1, z, act)
     return dict(name=f"{G}x(M={M}, N={N}, K={K})", fused=fused, split=split, flops=2.0 * G * M * N * K, keep=keep,
-                chained=chained, unchained=unchained, cflops=2.0 * G * M * N * (K + 768), fused6=fused6,
-                chained6=chained6, W1=W1)
+                chained=chained, unchained=unchained, cflops=2.0 * G * M * N * (K + 768))
 
 
 def timed(fn, iters):
@@ -108,13 +94,6 @@ def main():
         tc, tu = timed(c["chained"], args.iters), timed(c["unchained"], args.iters)
         print(f"{'':28s} + fc1 chained {tc:7.2f} us ({c['cflops'] / tc / 1e6:6.1f} TFLOP/s)   "
               f"fused + NT GEMM {tu:7.2f} us")
-        with ops.weight_planes(c["W1"]):
-            c["fused6"]()
-            c["chained6"]()
-            torch.cuda.synchronize()
-            t6, tc6 = timed(c["fused6"], args.iters), timed(c["chained6"], args.iters)
-        print(f"{'':28s} x6: fused {t6:7.2f} us ({c['flops'] / t6 / 1e6:6.1f} TFLOP/s)   + fc1 chained {tc6:7.2f} us "
-              f"({c['cflops'] / tc6 / 1e6:6.1f} TFLOP/s)")
 
 
 if __name__ == "__main__":
