@@ -869,6 +869,18 @@ def _zeros_for_none(grads, refs):
 
 
 # --------------------------------------------------------------------------- attention
+def _attn_bwd_kernel_name(hd, am, causal, drop, Tq, Tk, dq_part):
+    """The launch's main backward kernel as rocprofv3 names it (attention.hip launch_bwd): the
+    fused hd-16 kernel (T <= 256), the hd-32 key-block kernel (+ its dQ reduce), else the
+    split dq + dkdv pair (timed together, named by the dq kernel)."""
+    tf = lambda b: "true" if b else "false"  # noqa: E731
+    if hd == 16 and not am and Tq <= 256 and Tk <= 256:
+        return f"attn_bwd_fused_kernel<{tf(causal)}, {tf(drop)}>"
+    if hd == 32 and not am and dq_part:
+        return f"attn_bwd_kblk_kernel<{tf(causal)}, {tf(drop)}>"
+    return f"attn_bwd_dq_kernel<{hd}, {tf(am)}, {tf(causal)}, {tf(drop)}>"
+
+
 class KeyPaddingMask:
     """The SCA mask contract without the B*T^2 materialisation: per-clip key validity
     (B, Tk) as fp32 1/0 plus the causal flags.  Semantically identical to the additive masks
@@ -944,7 +956,8 @@ def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
                              sm[g].data_ptr(), sl[g].data_ptr(), ptr(key_valid), ptr(add_mask),
                              drop[1][g] if drop else 0, drop[0] if drop else 0.0, _mask_heads(add_mask)) for g in gs])
         fl = len(gs) * 4.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
-        with _timed("attn_fwd_kernel<%d>" % hd, fl):
+        tf = lambda b: "true" if b else "false"  # noqa: E731
+        with _timed(f"attn_fwd_kernel<{hd}, {tf(add_mask is not None)}, {tf(causal)}, {tf(drop)}>", fl):
             L.check(L.lib().sca_attn_fwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
                                          L.stream_handle()), "sca_attn_fwd")
     return o, sm, sl
@@ -978,7 +991,8 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
                              drop[1][g] if drop else 0, drop[0] if drop else 0.0, _mask_heads(add_mask))
             for g in gs])
         fl = len(gs) * 8.0 * B * H * hd * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
-        with _timed("attn_bwd(dq+dkdv)<%d>" % hd, fl):
+        with _timed(_attn_bwd_kernel_name(hd, add_mask is not None, causal, drop is not None, Tq, Tk,
+                                          part[0] is not None), fl):
             L.check(L.lib().sca_attn_bwd(len(gs), arr, B, H, Tq, Tk, hd, d, d, d, d, int(causal), int(plus_one),
                                          L.stream_handle()), "sca_attn_bwd")
     return dq, dk, dv
