@@ -380,6 +380,19 @@ typedef struct {
 #define SCA_GELU_MAX_PROBLEMS 8
 int sca_gelu_bwd(int nprob, const sca_gelu_bwd_problem* probs, long n, void* stream);
 
+/* Fixed-order sum of up to SCA_SUM_MAX_TERMS same-shaped tensors, n elements each:
+ * out = in[0] + in[1] + ... + in[nin-1] (left to right) — the gradient of a tensor read by
+ * several ops (the final x-stream map read by every merge layer, keypoint_module.py:181-187)
+ * in one launch per group instead of one autograd add per pair.  16-byte aligned.         */
+#define SCA_SUM_MAX_TERMS 8
+typedef struct {
+  const float* in[SCA_SUM_MAX_TERMS];
+  int nin;
+  float* out;
+} sca_sum_problem;
+#define SCA_SUM_MAX_PROBLEMS 8
+int sca_sum_tensors(int nprob, const sca_sum_problem* probs, long n, void* stream);
+
 /* Dropout (F.dropout, training mode) over contiguous (rows, cols) tensors:
  *   y[e] = x[e] * keep(seed, e) / (1 - p),  e = row * cols + col
  * keep() is a counter-based hash RNG (no state, no sequence): with

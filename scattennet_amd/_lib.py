@@ -99,6 +99,13 @@ class DropoutProblem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("seed", c_u64)]
 
 
+SUM_MAX_TERMS, SUM_MAX_PROBLEMS = 8, 8
+
+
+class SumProblem(ctypes.Structure):
+    _fields_ = [("inp", c_void_p * SUM_MAX_TERMS), ("nin", c_int), ("out", c_void_p)]
+
+
 class ReduceProblem(ctypes.Structure):
     _fields_ = [("inp", c_void_p), ("out", c_void_p), ("scale", c_float)]
 
@@ -138,6 +145,7 @@ EXPORTS = {
     "sca_softmax_rows_fwd": ([c_int, c_void_p, c_int, c_int, c_void_p], c_int),
     "sca_softmax_rows_bwd": ([c_int, c_void_p, c_int, c_int, c_void_p], c_int),
     "sca_gelu_bwd": ([c_int, c_void_p, c_long, c_void_p], c_int),
+    "sca_sum_tensors": ([c_int, c_void_p, c_long, c_void_p], c_int),
     "sca_dropout": ([c_int, c_void_p, c_long, c_int, c_float, c_void_p], c_int),
     "sca_dropout_offset": ([c_void_p], c_int),
     "sca_reduce_rows": ([c_int, c_void_p, c_int, c_int, c_int, c_long, c_long, c_int, c_void_p], c_int),

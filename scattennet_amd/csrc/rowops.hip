@@ -488,6 +488,27 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const GeluArgs a) {
     P.dz[e] = P.dy[e] * gelu_erf_grad(P.z[e]);
 }
 
+// ------------------------------------------------------------------------------ fixed-order tensor sum
+struct SumArgs {
+  sca_sum_problem p[SCA_SUM_MAX_PROBLEMS];
+  long n;
+};
+
+__global__ __launch_bounds__(256) void sum_tensors_kernel(const SumArgs a) {
+  const sca_sum_problem& P = a.p[blockIdx.y];
+  const long n4 = a.n / 4;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n4; e += (long)gridDim.x * 256) {
+    f32x4 s = ld4(P.in[0] + 4 * e);
+    for (int j = 1; j < P.nin; ++j) s += ld4(P.in[j] + 4 * e);
+    st4(P.out + 4 * e, s);
+  }
+  for (long e = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; e < a.n; e += (long)gridDim.x * 256) {
+    float s = P.in[0][e];
+    for (int j = 1; j < P.nin; ++j) s += P.in[j][e];
+    P.out[e] = s;
+  }
+}
+
 // ------------------------------------------------------------------------------ MaxPool1d(2,2) over T
 struct PoolArgs {
   sca_pool_problem p[SCA_POOL_MAX_PROBLEMS];
@@ -943,6 +964,35 @@ extern "C" int sca_gelu_bwd(int nprob, const sca_gelu_bwd_problem* probs, long n
   dim3 grid((unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048), nprob);
   hipLaunchKernelGGL(gelu_bwd_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gelu_bwd: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_sum_tensors(int nprob, const sca_sum_problem* probs, long n, void* stream) {
+  if (nprob < 1 || nprob > SCA_SUM_MAX_PROBLEMS || n < 0 || !probs) {
+    sca_set_error("sca_sum_tensors: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  SumArgs a;
+  for (int i = 0; i < nprob; ++i) {
+    const sca_sum_problem& P = probs[i];
+    uintptr_t al = reinterpret_cast<uintptr_t>(P.out);
+    bool ok = P.nin >= 1 && P.nin <= SCA_SUM_MAX_TERMS && P.out;
+    for (int j = 0; ok && j < P.nin; ++j) {
+      ok = P.in[j] != nullptr;
+      al |= reinterpret_cast<uintptr_t>(P.in[j]);
+    }
+    if (!ok || (al & 15)) {
+      sca_set_error("sca_sum_tensors: 1..8 non-null, 16-byte aligned inputs and an output per problem");
+      return SCA_ERR_ARG;
+    }
+    a.p[i] = P;
+  }
+  if (n == 0) return SCA_OK;
+  a.n = n;
+  const long blocks = (n / 4 + 255) / 256;
+  dim3 grid((unsigned)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024), nprob);
+  hipLaunchKernelGGL(sum_tensors_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_sum_tensors: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
 

@@ -163,6 +163,7 @@ def sca_grouped(scas, xs, ys, attention_mask):
     else:
         s = _self_stack(scas, s, self_mask, L)
     c = ce
+    s_for = None
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
         if i == 0 and branch is not None:
@@ -170,8 +171,12 @@ def sca_grouped(scas, xs, ys, attention_mask):
             ops.note_join(main, branch)
             for t in s:
                 t.record_stream(main)
+        if i == 0:
+            # every merge layer reads the final x-stream map: one fan-out, so that its L
+            # incoming gradients are summed in one grouped launch after the last merge's backward
+            s_for = ops.fan_out(s, L) if not library.compiling() else [s] * L
         nxt = qkv_request([m.causal_attn_layers[i + 1] for m in scas]) if i + 1 < L else None
-        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s, cross_mask, nxt=nxt)
+        c = coordinates_merge_grouped([m.coordinates_merge[i] for m in scas], c, s_for[i], cross_mask, nxt=nxt)
     return c, s
 
 

@@ -7,6 +7,8 @@ config-2 shape (B=8, T=256, d=256) a single stream's GEMM is only 2048 x 256 x 2
 Activations are contiguous (B, T, C) fp32 on the GPU, viewed as (M = B*T, C) row-major.
 Parameters keep the nn.Linear / nn.LayerNorm layouts of the reference (W is [out, in]).
 """
+import ctypes
+
 import torch
 from torch.autograd import Function
 
@@ -854,6 +856,64 @@ def _weight_grads(items):
     for p, k, w, tl in launches:
         gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl)
     return out
+
+
+def sum_tensors(groups):
+    """groups: [(out, [in_0, in_1, ...])] same-shaped contiguous fp32 tensors: out = sum of the
+    ins in list order (sca_sum_tensors, one launch per 8 groups)."""
+    if not groups:
+        return
+    n = groups[0][0].numel()
+    for c in range(0, len(groups), L.SUM_MAX_PROBLEMS):
+        chunk = groups[c:c + L.SUM_MAX_PROBLEMS]
+        probs = []
+        for out, ins in chunk:
+            if len(ins) > L.SUM_MAX_TERMS:
+                raise ValueError(f"sum_tensors: at most {L.SUM_MAX_TERMS} terms")
+            arr = (ctypes.c_void_p * L.SUM_MAX_TERMS)(*[t.data_ptr() for t in ins])
+            probs.append(L.SumProblem(arr, len(ins), out.data_ptr()))
+        L.check(L.lib().sca_sum_tensors(len(probs), (L.SumProblem * len(probs))(*probs), n, L.stream_handle()),
+                "sca_sum_tensors")
+
+
+class FanOut(Function):
+    """The same G tensors handed to n consumers: forward returns n aliases of each (views);
+    backward sums each tensor's n incoming gradients in one grouped launch (sca_sum_tensors,
+    fixed order) instead of autograd's n - 1 pairwise adds per tensor as they arrive — the
+    final x-stream map read by every merge layer (keypoint_module.py:181-187)."""
+
+    @staticmethod
+    def forward(ctx, n, G, *xs):
+        ctx.n, ctx.G = n, G
+        return tuple(x.view_as(x) for _ in range(n) for x in xs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        n, G = ctx.n, ctx.G
+        groups, outs = [], []
+        for g in range(G):
+            terms = [t.contiguous() for t in (gs[i * G + g] for i in range(n)) if t is not None]
+            if not terms:
+                outs.append(None)
+            elif len(terms) == 1:
+                outs.append(terms[0])
+            else:
+                o = torch.empty_like(terms[0])
+                groups.append((o, terms))
+                outs.append(o)
+        sum_tensors(groups)
+        return (None, None) + tuple(outs)
+
+
+_FAN_OUT = True
+
+
+def fan_out(xs, n):
+    """n lists of aliases of the G tensors xs (FanOut); [xs] * n when n < 2 or not on the HIP path."""
+    if not _FAN_OUT or n < 2 or _LIBRARY_MODE or not torch.is_grad_enabled() or not any(x.requires_grad for x in xs):
+        return [list(xs)] * n
+    out = FanOut.apply(n, len(xs), *xs)
+    return [list(out[i * len(xs):(i + 1) * len(xs)]) for i in range(n)]
 
 
 def _flat(x):

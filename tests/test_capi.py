@@ -43,6 +43,7 @@ _STRUCTS = {  # C struct in include/scatten.h -> ctypes mirror in scattennet_amd
     "sca_coord_map_problem": "CoordMapProblem", "sca_coord_map_bwd_problem": "CoordMapBwdProblem",
     "sca_dropout_problem": "DropoutProblem", "sca_gemm_ln_problem": "GemmLnProblem",
     "sca_gemm_lnb_problem": "GemmLnbProblem", "sca_gemm_chain_pass": "ChainPass",
+    "sca_sum_problem": "SumProblem",
 }
 
 
