@@ -167,7 +167,7 @@ def attention_block(xq: Tensor, xkv: Optional[Tensor], params: List[Tensor], ln_
     ts = [xq] + _opt(xkv if kind == "cross" else None) + list(params) + ([ln_weight, ln_bias] if fused else [])
     with ops.library_mode():
         (y,) = ops.AttentionBlock.forward(ctx, 1, kind, num_heads, scale, plus_one, key_valid, add_mask, resid, 0.0,
-                                          ln_eps if fused else None, None, None, 0.0, *ts)
+                                          ln_eps if fused else None, None, 0.0, *ts)
         sv = ctx.saved_tensors
         i = 2 + 1 + (1 if kind == "cross" else 0) + 8
         inter = list(sv[i:i + 6])
@@ -221,7 +221,7 @@ def attention_block_backward(dy: Tensor, xq: Tensor, xkv: Optional[Tensor], para
     cross = kind == "cross"
     ctx = _Ctx()
     ctx.G, ctx.kind, ctx.H, ctx.scale, ctx.plus_one, ctx.has_resid = 1, kind, num_heads, scale, plus_one, resid
-    ctx.attn_drop, ctx.drop_p, ctx.seeds, ctx.ln = None, None, 0.0, [None], fused
+    ctx.attn_drop, ctx.drop_p, ctx.seeds, ctx.ln = None, 0.0, [None], fused
     ctx.bet = (ln_bias,) if fused else ()
     ctx.lnsaved = ctx.lnprev = None
     sv = [key_valid, add_mask, xq] + _opt(xkv if cross else None) + list(params) + list(saved[:6])
@@ -234,7 +234,7 @@ def attention_block_backward(dy: Tensor, xq: Tensor, xkv: Optional[Tensor], para
             dy, dg, db = _ln_plain_bwd(dy, saved[6], ln_weight, ln_bias, saved[7], saved[8])
             dln = [dg, db]
         g = ops.AttentionBlock.backward(ctx, dy.contiguous())
-    return [t for t in g[13:] if t is not None] + dln
+    return [t for t in g[12:] if t is not None] + dln
 
 
 @attention_block_backward.register_fake

@@ -648,6 +648,7 @@ import os as _os
 
 _WGRAD_SIDE = True
 _BRANCH_SIDE = True  # branch-stream weight grads on their own side stream
+_EARLY_FORK = True   # fork the weight gradients before the layer's input-gradient launch
 _side_streams = {}
 _join_pending = {}
 
@@ -767,7 +768,23 @@ def _queue_join(main, side):
     torch.autograd.Variable._execution_engine.queue_callback(_join)
 
 
-def weight_grads(items, M=None, extra=None):
+def wgrad_ready():
+    """Mark, on the current stream, the point where the inputs of a layer's weight gradients are
+    ready — before the layer's last input-gradient launch.  weight_grads(..., ready=ev) forks
+    its side stream from this point, so that in the captured graph the input-gradient launch is
+    the first child of the producing node and the weight gradients the second: hipGraph keeps a
+    node's first child on the parent's queue and starts a new queue list for the others, which
+    keeps the critical chain on one hardware queue (forking after the input-gradient launch made
+    the weight gradients its first child and moved the chain to the other queue at every layer,
+    behind whatever that queue held)."""
+    if not _EARLY_FORK or not _WGRAD_SIDE or _LIBRARY_MODE:
+        return None
+    ev = torch.cuda.Event()
+    ev.record()
+    return ev
+
+
+def weight_grads(items, M=None, extra=None, ready=None):
     """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
     the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
 
@@ -803,7 +820,10 @@ def weight_grads(items, M=None, extra=None):
         side = _side_stream(dev, 1)
     else:
         side = _side_stream(dev)
-    side.wait_stream(main)  # dY and X are ready on the main stream
+    if ready is not None:
+        side.wait_event(ready)  # dY and X were ready at this point of the main stream
+    else:
+        side.wait_stream(main)  # dY and X are ready on the main stream
     note_fork(side, main, "weight-gradient side stream")
     for it in items:  # keep their memory from being reused by the main stream too early
         it[0].record_stream(side)
@@ -1199,6 +1219,7 @@ class AttentionBlock(Function):
                 probs.append(_prob([_seg(dqf, Wq, d, d, d), _seg(dkf, Wk, d, d, d), _seg(dvf, Wv, d, d, d)],
                                    gx, B * T, d, d, resid=r, ldr=d))
             dxq.append(gx)
+        ready = wgrad_ready()
         if ctx.lnprev is not None:
             hand_off(ctx.lnprev, dxq, *gemm_lnb(probs, ctx.lnprev))
             ctx.lnprev = None
@@ -1213,7 +1234,7 @@ class AttentionBlock(Function):
             items += [(_flat(dq[g]), xf, 1.0, Wq, bq), (_flat(dk[g]), kf, 1.0, Wk, bk),
                       (_flat(dv[g]), kf, 1.0, Wv, bv, 1.0 / av),
                       (_flat(dyo[g]), _flat(o[g]), 1.0, Wo[g], bo[g])]
-        wg = weight_grads(items, extra=ln_finish)
+        wg = weight_grads(items, extra=ln_finish, ready=ready)
         dW, dWo, dbo = [], [], []
         for g in range(G):
             for j in range(3):
@@ -1262,8 +1283,9 @@ class LinearResidual(Function):
             dx = torch.empty_like(x[g])
             probs.append(_prob([_seg(_flat(dys[g]), W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
             dxs.append(dx)
+        ready = wgrad_ready()
         gemm(L.GEMM_NN, probs)
-        wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
+        wg = weight_grads([(_flat(dys[g]), _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)], ready=ready)
         return (None, None) + tuple(dxs) + tuple(w for w, _ in wg) + tuple(bb for _, bb in wg) + \
             (tuple(dys) if ctx.has_r else ())
 
@@ -1358,6 +1380,7 @@ class FeedForwardResidual(Function):
         # dx = dz W1 + dy   (residual); with `lnprev` the input's LayerNorm backward rides in
         # the same launch (sca_gemm_lnb)
         dx = [torch.empty_like(x[g]) for g in range(G)]
+        ready = wgrad_ready()
         probs = [_prob([_seg(dz[g], W1[g], F_, d, F_)], dx[g], M, d, d,
                        resid=_flat(dys[g]) if ctx.has_r else None, ldr=d) for g in range(G)]
         if ctx.lnprev is not None:
@@ -1368,7 +1391,7 @@ class FeedForwardResidual(Function):
         items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], ctx.b2[g] if ctx.b2[g] is not None else True)
                  for g in range(G)] + \
                 [(dz[g], _flat(x[g]), 1.0, W1[g], ctx.b1[g] if ctx.b1[g] is not None else True) for g in range(G)]
-        wg = weight_grads(items, extra=ln_finish)
+        wg = weight_grads(items, extra=ln_finish, ready=ready)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
         return (None,) * 5 + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \
@@ -1633,8 +1656,9 @@ class LinearGelu(Function):
             dx = torch.empty_like(x[g])
             probs.append(_prob([_seg(dz[g], W[g], n_out, n_in, n_out)], dx, M, n_in, n_in))
             dxs.append(dx)
+        ready = wgrad_ready()
         gemm(L.GEMM_NN, probs)
-        wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)])
+        wg = weight_grads([(dz[g], _flat(x[g]), 1.0, W[g], ctx.b[g]) for g in range(G)], ready=ready)
         return (None, None) + tuple(dxs) + tuple(w for w, _ in wg) + tuple(bb for _, bb in wg) + \
             (tuple(dys) if ctx.has_r else ())
 
