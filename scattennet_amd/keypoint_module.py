@@ -144,33 +144,15 @@ def sca_grouped(scas, xs, ys, attention_mask):
     causal_mask = self_mask.causal_view()  # model/utils.py:15-28 (same key validity, +1 on j <= i)
     cross_mask = self_mask  # create_attention_mask(tgt_len=T) — same key padding
     L = len(scas[0].self_attn_layers)
-    branch = _branch_stream(se[0].device) if (L > 0 and _BRANCH_OVERLAP and se[0].is_cuda and
-                                              not library.compiling()) else None
-    s = se
-    if branch is not None:
-        # The self stack reads only the x stream and the first causal layer only the y stream:
-        # the self stack runs on a second stream while causal layer 0 runs on this one (host
-        # order, and so dropout-seed order, stays the reference's; each backward node follows
-        # its forward's stream).
-        main = torch.cuda.current_stream(se[0].device)
-        _branch_stream(se[0].device, main)  # records the join target of the branch
-        branch.wait_stream(main)
-        ops.note_fork(branch, main, "branch stream")
-        for t in list(se) + [self_mask.key_valid]:
-            t.record_stream(branch)
-        with torch.cuda.stream(branch):
-            s = _self_stack(scas, s, self_mask, L)
-    else:
-        s = _self_stack(scas, s, self_mask, L)
+    # one stream: a second stream for the self stack (concurrent with causal layer 0) was
+    # -13 % at config 3 and -2.6 % at config 2 — the graph executor runs a forked branch's
+    # queue list behind the main list, so the weight gradients queued behind it waited for the
+    # whole backward
+    s = _self_stack(scas, se, self_mask, L)
     c = ce
     s_for = None
     for i in range(L):
         c = coordinate_attention_grouped([m.causal_attn_layers[i] for m in scas], c, causal_mask)
-        if i == 0 and branch is not None:
-            main.wait_stream(branch)
-            ops.note_join(main, branch)
-            for t in s:
-                t.record_stream(main)
         if i == 0:
             # every merge layer reads the final x-stream map: one fan-out, so that its L
             # incoming gradients are summed in one grouped launch after the last merge's backward
@@ -187,8 +169,6 @@ def _self_stack(scas, s, mask, L):
     return s
 
 
-_BRANCH_OVERLAP = True
-_branch_stream = ops.branch_stream
 
 
 # --------------------------------------------------------------------------- A1 + A2 + A11 + A12

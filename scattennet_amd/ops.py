@@ -638,49 +638,31 @@ def params_produced(ps):
 
 # ---- weight-gradient side stream -------------------------------------------------------
 # The weight/bias-gradient GEMMs of a layer do not feed the rest of the backward pass, so
-# they run on a side HIP stream, concurrently with the input-gradient GEMMs and attention
-# backward of the same and the next layers (each launch alone fills the chip poorly at
-# these sizes).  A callback queued on the autograd engine joins the side stream into the
-# caller's stream when backward() completes, so .grad is safe to read afterwards exactly as
-# with a single stream (the same mechanism torch DDP uses).  Captured into hipGraphs as a
-# fork/join.
-import os as _os
+# they go to a side HIP stream, forked from the point where their inputs are ready
+# (wgrad_ready) and joined into the caller's stream by a callback queued on the autograd
+# engine when backward() completes, so .grad is safe to read afterwards exactly as with a
+# single stream (the same mechanism torch DDP uses).  Captured into the step's hipGraph as
+# fork/join edges: the critical chain stays on one hardware queue and the weight gradients
+# fill the other — in practice behind the chain's second half (the executor's queue lists,
+# DESIGN.md §9).
 
 _WGRAD_SIDE = True
-_BRANCH_SIDE = True  # branch-stream weight grads on their own side stream
 _EARLY_FORK = True   # fork the weight gradients before the layer's input-gradient launch
 _side_streams = {}
 _join_pending = {}
 
 
-def _side_stream(device, which=0):
-    st = _side_streams.get((device, which))
+def _side_stream(device):
+    st = _side_streams.get(device)
     if st is None:
         st = torch.cuda.Stream(device=device)
-        _side_streams[(device, which)] = st
-    return st
-
-
-_branch_streams = {}
-_branch_origin = {}  # branch stream ptr -> the stream it was forked from (its join target)
-
-
-def branch_stream(device, origin=None):
-    """Second compute stream for independent forward branches (the x-stream self stack,
-    keypoint_module.sca_grouped); autograd runs their backward nodes on it as well.
-    `origin`: the stream the branch forks from and is joined back into."""
-    st = _branch_streams.get(device)
-    if st is None:
-        st = torch.cuda.Stream(device=device)
-        _branch_streams[device] = st
-    if origin is not None:
-        _branch_origin[st.cuda_stream] = origin
+        _side_streams[device] = st
     return st
 
 
 class ForkLedger:
     """Host-side record of the stream forks and joins the hot path makes — weight-gradient side
-    streams (weight_grads), the branch stream (keypoint_module.sca_grouped), RCCL's stream
+    streams (weight_grads), RCCL's stream
     (dp.GradBuckets) — checked at the end of a graph capture: every stream forked during the
     capture must afterwards be joined DIRECTLY into the capture's origin stream.  (DESIGN §7,
     constraint (1): a forked stream joined into another forked stream that then joins the
@@ -807,19 +789,7 @@ def weight_grads(items, M=None, extra=None, ready=None):
         return run()
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
-    join_into = main
-    br = _branch_streams.get(dev)
-    if br is not None and br.cuda_stream == main.cuda_stream:
-        # on the branch stream (the self stack's backward): fork a second side stream from it,
-        # joined into the stream the branch itself was forked from — the branch has already
-        # been joined back by autograd when the join callback runs (a wait queued into it then
-        # would be an unjoined fork under graph capture)
-        join_into = _branch_origin.get(br.cuda_stream)
-        if join_into is None or not _BRANCH_SIDE:
-            return run()
-        side = _side_stream(dev, 1)
-    else:
-        side = _side_stream(dev)
+    side = _side_stream(dev)
     if ready is not None:
         side.wait_event(ready)  # dY and X were ready at this point of the main stream
     else:
@@ -832,7 +802,7 @@ def weight_grads(items, M=None, extra=None, ready=None):
         t.record_stream(side)
     with torch.cuda.stream(side):
         out = run()
-    _queue_join(join_into, side)
+    _queue_join(main, side)
     return out
 
 

@@ -1,7 +1,7 @@
 """Host cost of launching the captured step: time N graph.replay() calls without a sync
 (host submission) against the time until the GPU is done (config 2 unless --workload).
 
-    python tools/replay_probe.py [--workload cfg2] [--n 20] ["keypoint_module._BRANCH_OVERLAP=False" ...]
+    python tools/replay_probe.py [--workload cfg2] [--n 20] ["ops._EARLY_FORK=False" ...]
 """
 import os
 import sys
