@@ -131,11 +131,42 @@ __global__ __launch_bounds__(512) void ring_kernel(const Args a) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + S - 1 < total) issue(t + S - 1, (t + S - 1) % S);
+    if (SG < 4 && t + S - 1 < total) issue(t + S - 1, (t + S - 1) % S);
     if (MODE != 1) {
       const char* As = smem + (t % S) * STAGE;
       const char* Bs = As + A_BYTES;
       f32x4 fa[4], fb[4];
+      if (SG >= 4) {  // DMA of slice t+S-1 issued under the MFMAs: after group 0 (4) / spread (5)
+#define SB __builtin_amdgcn_sched_barrier(0)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          fa[g] = frag(As, 0, g, lane);
+          fb[g] = frag(Bs, 32 * wave, g, lane);
+        }
+        SB;
+        const bool more = t + S - 1 < total;
+        char* base = smem + ((t + S - 1) % S) * STAGE;
+        const long kk = (long)(t + S - 1) * BK;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc = mfma32(fa[g][j], fb[g][j], acc);
+          SB;
+          if (MODE != 2 && more) {
+            if (SG == 4 && g == 0) {
+              if (has_a) dma(pa + kk, base + wave * PIECE);
+#pragma unroll
+              for (int c = 0; c < 4; ++c) dma(pb[c] + kk, base + A_BYTES + (4 * wave + c) * PIECE);
+            } else if (SG == 5) {
+              if (g == 0 && has_a) dma(pa + kk, base + wave * PIECE);
+              dma(pb[g] + kk, base + A_BYTES + (4 * wave + g) * PIECE);
+            }
+          }
+          SB;
+        }
+#undef SB
+        continue;
+      }
       if (SG == 3) {  // untracked reads, partial waits
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -607,6 +638,8 @@ int main(int argc, char** argv) {
   report("mode 3: direct registers, D=4", time_it([&] { direct_kernel<3, 4><<<grid, 512>>>(a); }, 50), true);
   report("mode 4: A ring + B direct, D=2", time_it([&] { direct_kernel<4, 2><<<grid, 512>>>(a); }, 50), true);
   report("mode 4: A ring + B direct, D=3", time_it([&] { direct_kernel<4, 3><<<grid, 512>>>(a); }, 50), true);
+  report("mode 0, DMA after MFMA group 0 (SG4)", time_it([&] { ring_kernel<0, 4><<<grid, 512>>>(a); }, 50), true);
+  report("mode 0, DMA spread over MFMA groups (SG5)", time_it([&] { ring_kernel<0, 5><<<grid, 512>>>(a); }, 50), true);
   report("mode 0 + all reads first (SG1)", time_it([&] { ring_kernel<0, 1><<<grid, 512>>>(a); }, 50), true);
   report("mode 0 + staged reads (SG2)", time_it([&] { ring_kernel<0, 2><<<grid, 512>>>(a); }, 50), true);
   report("mode 2 + all reads first (SG1)", time_it([&] { ring_kernel<2, 1><<<grid, 512>>>(a); }, 50), false);
