@@ -564,6 +564,9 @@ _SPLITK_MAX = 8
 _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per CU
 
 
+_TNK_TILES_PER_PROBLEM = 48
+
+
 def _splitk_for(M_red, n_out_tiles):
     """Split the long reduction (rows of the batch) of weight-gradient GEMMs: the split that
     fills whole rounds of the LDS-DMA kernel's 3 workgroups per CU (768 slots) best, each
@@ -828,11 +831,13 @@ def _weight_grads(items):
             tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
             sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
             tile = 0
-            if len(sub) >= 8 and tiles >= 256:
-                # many-problem launches (an attention block's q/k/v/o of every stream): the
-                # k-split outer-product kernel at split-K 2 (tools/tn_bench.py: 16 x (256 x 256,
-                # K = 2048) 0.59-0.61 of peak vs 0.57 for the 64x64 LDS-DMA kernel at split 3)
-                tile, sk = 36, 2
+            if (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
+                # many-problem launches (an attention block's q/k/v/o of every stream) and big
+                # weights (an FFN's 768 x 256): the k-split outer-product kernel at split-K 2
+                # (tools/tn_bench.py: 16 x (256 x 256, K = 2048) 0.59-0.61 of peak vs 0.57 for
+                # the 64x64 LDS-DMA kernel at split 3; the FFN launches at split 2 instead of 4
+                # write half the partial slabs, same step time; profiles/r04_probe/ab_tnk_ffn.txt)
+                tile, sk = 36, min(sk, 2)
             probs, wsz = [], 0
             for i in sub:
                 dY, X, alpha, W, _, bscale = items[i]
