@@ -722,7 +722,10 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
 // 4c .. 4c+3 (g = lane >> 4, c = lane & 15).  Epilogue, split-K slabs and in-launch combine
 // as gemm_glds_kernel (same 32x32 quadrant row layout after the reduction).
 constexpr int TNK_PLD = 68;  // partial-tile row stride (floats): 16-B shift per row
-constexpr int TNK_RED = 4 * 64 * TNK_PLD * 4 + 4 * 64 * 4;  // 4 partial tiles + 4 bias partial rows
+// 2 partial tiles + 4 bias partial rows: the waves' tiles are summed in two rounds (waves 2, 3
+// hand theirs to waves 0, 1, which then publish the pair sums), so the reduction fits in the
+// 48-KB ring and three workgroups share a CU (the one-round form took 70 KB: two per CU)
+constexpr int TNK_RED = 2 * 64 * TNK_PLD * 4 + 4 * 64 * 4;
 
 // SUB: K slices per ring stage (one wait + barrier per SUB x 32 k rows)
 template <int S, int SUB>
@@ -842,16 +845,11 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
     }
   }
 
-  // the 4 waves' partial tiles (and bias rows) through LDS, summed in fixed order per quadrant
+  // the 4 waves' partial tiles (and bias rows) through LDS, summed in a fixed order:
+  // (wave 0 + wave 2) + (wave 1 + wave 3), in two rounds over two tile slots
   __syncthreads();  // the ring is free
   float* red = reinterpret_cast<float*>(smem);
-  float* mine = red + wave * 64 * TNK_PLD;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      st4(mine + (16 * g + 4 * r + i) * TNK_PLD + 4 * c, f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]});
-  float* bred = red + 4 * 64 * TNK_PLD;
+  float* bred = red + 2 * 64 * TNK_PLD;
   if (do_bias) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -860,6 +858,33 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
     }
     if (g == 0) st4(bred + wave * 64 + 4 * c, bs4);
   }
+  float* slot = red + (wave & 1) * 64 * TNK_PLD;
+  if (wave >= 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        st4(slot + (16 * g + 4 * r + i) * TNK_PLD + 4 * c, f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]});
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 t = ld4(slot + (16 * g + 4 * r + i) * TNK_PLD + 4 * c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j][r] += t[j];
+      }
+  }
+  __syncthreads();  // the partner tiles are consumed
+  if (wave < 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        st4(slot + (16 * g + 4 * r + i) * TNK_PLD + 4 * c, f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]});
+  }
   __syncthreads();
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const float alpha = P.seg[0].alpha;
@@ -867,8 +892,7 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
 #pragma unroll
   for (int i4 = 0; i4 < 4; ++i4) {
     const int e = (wm + (lane >> 3) + 8 * i4) * TNK_PLD + wn + 4 * (lane & 7);
-    rows[i4] = ((ld4(red + e) + ld4(red + 64 * TNK_PLD + e)) + ld4(red + 2 * 64 * TNK_PLD + e)) +
-               ld4(red + 3 * 64 * TNK_PLD + e);
+    rows[i4] = ld4(red + e) + ld4(red + 64 * TNK_PLD + e);
     if (alpha != 1.f) rows[i4] *= alpha;
   }
   const bool fused_k = splitk > 1 && args.counters != nullptr;
