@@ -23,7 +23,7 @@ w = torch.randn(2048, 2048, device=dev) / 45
 b = torch.randn(1024, 1024, device=dev)
 w2 = torch.randn(1024, 1024, device=dev) / 32
 side = torch.cuda.Stream()
-if MODE.startswith("lib"):
+if MODE.startswith("lib") or MODE == "mmlib":
     # our kernels: the chain = fused GEMM + LayerNorm launches (1 workgroup / CU, 147 KB LDS), the
     # side = k-split weight-gradient launches (tools/gemm_ln_bench.py / the step's shapes)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -50,8 +50,10 @@ if MODE.startswith("lib"):
         ops.gemm_ln(probs, lns, 1e-5)
         return x
 
+    SIDE_TILE = 36 if MODE == "lib" else 0  # lib: k-split kernel (70 KB LDS); lib32: LDS-DMA 64x64 (32 KB)
+
     def side_op(y):
-        ops.gemm(L.GEMM_TN, tprobs, splitk=2, ws=ws, tile=36)
+        ops.gemm(L.GEMM_TN, tprobs, splitk=2, ws=ws, tile=SIDE_TILE)
         return y
 
 
@@ -60,11 +62,11 @@ def step():
     main = torch.cuda.current_stream()
     ys = []
     for i in range(N):
-        if MODE in ("each", "lib") and i > F:
+        if MODE in ("each", "lib", "lib32", "libmm", "mmlib") and i > F:
             ev = torch.cuda.Event()
             ev.record()
-        x = chain_op(x) if MODE.startswith("lib") else torch.mm(x, w)
-        if (MODE == "one" and i == F) or (MODE in ("each", "lib") and i > F):
+        x = chain_op(x) if MODE.startswith("lib") else torch.mm(x, w)  # libmm: our chain, torch.mm side
+        if (MODE == "one" and i == F) or (MODE in ("each", "lib", "lib32", "libmm", "mmlib") and i > F):
             if MODE == "one":
                 ev = torch.cuda.Event()
                 ev.record()
@@ -72,7 +74,8 @@ def step():
             with torch.cuda.stream(side):
                 y = b
                 for _ in range(S):
-                    y = side_op(y) if MODE.startswith("lib") else torch.mm(y, w2)
+                    y = side_op(y) if (MODE.startswith("lib") and MODE != "libmm") or MODE == "mmlib" \
+                        else torch.mm(y, w2)
                 ys.append(y)
     main.wait_stream(side)
     return x, ys
