@@ -2,12 +2,12 @@
 tile and split-K, interleaved in one process; every variant is first checked against a
 float64 host product (dW and the fused bias gradient).
 
-    python tools/tn_bench.py [--iters 20] [--rounds 3] [--tiles 21,30,31] [--splits 1,2,3,4]
+    python tools/tn_bench.py [--iters 20] [--rounds 3] [--tiles 21,36,37] [--splits 1,2,3,4]
 
 Shapes (per step: 12 + 16 launches): the attention blocks' q/k/v/o of 4 streams =
 16 x (256 x 256, K = 2048); the FFN fc1 4 x (768 x 256) and fc2 4 x (256 x 768), K = 2048.
-Tiles: 21 = gemm_glds_kernel<TN, 2> (64x64, 4 waves: the round-2 default), 30..35 =
-gemm_tn_kernel variants (csrc/gemm.hip TN0..TN5)."""
+Tiles: 21 = gemm_glds_kernel<TN, 2> (64x64 LDS-DMA, 4 waves), 36 / 37 = gemm_tnk_kernel<3 / 4, 1>
+(the k-split outer-product kernel, 3- / 4-stage ring)."""
 import argparse
 import os
 import sys
@@ -17,10 +17,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-NAMES = {21: "glds64", 30: "T64s4", 31: "T64+4L", 32: "T64pf", 33: "T64pf+4L", 34: "T128x64pf+4L", 35: "T64s3pf+4L",
-         36: "TNKs3", 37: "TNKs4", 38: "TNKs3pf", 39: "TNKs4pf", 40: "probe-noDMA", 41: "probe-pf-noDMA", 42: "probe-noDMA-nobar", 43: "probe-DMA-noMFMA"}
-TILE_BM = {21: (64, 64), 30: (64, 64), 31: (64, 64), 32: (64, 64), 33: (64, 64), 34: (128, 64), 35: (64, 64),
-           36: (64, 64), 37: (64, 64), 38: (64, 64), 39: (64, 64), 40: (64, 64), 41: (64, 64), 42: (64, 64), 43: (64, 64)}
+NAMES = {21: "glds64", 36: "TNKs3", 37: "TNKs4"}
+TILE_BM = {21: (64, 64), 36: (64, 64), 37: (64, 64)}
 
 
 def make_case(name, shapes, Mr=2048):
