@@ -17,8 +17,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-NAMES = {21: "glds64", 36: "TNKs3", 37: "TNKs4"}
-TILE_BM = {21: (64, 64), 36: (64, 64), 37: (64, 64)}
+NAMES = {1: "reg64", 5: "reg64s1", 7: "reg128x64", 20: "glds64s3", 21: "glds64", 22: "glds64s4", 36: "TNKs3", 37: "TNKs4"}
+TILE_BM = {1: (64, 64), 5: (64, 64), 7: (128, 64), 20: (64, 64), 21: (64, 64), 22: (64, 64), 36: (64, 64), 37: (64, 64)}
 
 
 def make_case(name, shapes, Mr=2048):
