@@ -9,6 +9,12 @@ the step includes the RCCL gradient all-reduce.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2] [--no-graph]
 
+--gpus N > 1 without a launcher (WORLD_SIZE unset): this process starts N rank processes of
+the same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their
+environment, one GPU each) and exits with their status; it never touches the GPU itself.
+Under torch.distributed.run (WORLD_SIZE set) --gpus must agree with WORLD_SIZE.
+SCA_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin).
+
 Prints ONE JSON line on rank 0 (contract in the build instructions), including:
   roofline      the dominant kernel's algorithmic FLOP rate (HIP events around each of its
                 launches in an instrumented eager step after the timed region) vs fp32 MFMA peak
@@ -43,7 +49,7 @@ HBM_PEAK_GBS = 8000.0
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default: WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg2", choices=sorted(W.WORKLOADS))
@@ -55,13 +61,49 @@ def parse():
     return ap.parse_args()
 
 
-def main():
-    args = parse()
+def spawn_ranks(n):
+    """Start n rank processes of this bench command and wait for them (the parent imports torch
+    but makes no GPU call: torch.cuda.device_count() does not initialise the device).  Returns
+    the first non-zero exit status, else 0."""
+    import signal
+    import socket
+    import subprocess
+    backend = os.environ.get("SCA_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {ndev} GPU(s) visible; RCCL needs one GPU per rank "
+                         "(SCA_DIST_BACKEND=gloo rehearses several ranks per GPU)")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            rc = p.poll()
+            if rc is None:
+                continue
+            pending.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in pending:  # one rank failed: the others would wait in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return status
+
+
+def main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
     if os.environ.get("SCA_DIST_BACKEND", "nccl") != "nccl":  # rehearsal: ranks may share a GPU
-        local %= max(1, torch.cuda.device_count())
+        local %= max(1, ndev)
     # SCA_DP_FORCE=1 (under torch.distributed.run): the data-parallel path at world size 1 —
     # rehearses the captured bucketed RCCL all-reduces on a one-GPU box
     use_dp = world > 1 or ("MASTER_ADDR" in os.environ and os.environ.get("SCA_DP_FORCE", "0") != "0")
@@ -223,7 +265,7 @@ def main():
             "config": {"workload": f"{args.workload}: " + describe(w), "clips_per_gpu": w["B"], "frames": w["T"],
                        "joints": w["K_all"], "streams": w["groups"], "d_model": w["d"], "heads": w["H"],
                        "layers": w["L"], "dropout": args.dropout, "hipgraph": graph is not None,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "devices": min(world, max(1, ndev))},
             "ms_per_step_median": round(ms_median, 4),
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -390,4 +432,10 @@ def cpu_baseline(w, model, budget_s):
 
 
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    _ws = os.environ.get("WORLD_SIZE")
+    if _ws is None and (_args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(_args.gpus))
+    if _ws is not None and _args.gpus is not None and _args.gpus != int(_ws):
+        raise SystemExit(f"bench.py: --gpus {_args.gpus} disagrees with WORLD_SIZE={_ws}")
+    main(_args)

@@ -169,6 +169,9 @@ int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_gemm_ln_prob
  * chained passes or not — the rule the launcher applies (SCA_GEMM_LN_BM overrides without
  * chained passes); hosts use it to name the kernel variant in their profiles. */
 int sca_gemm_ln_rows(int nprob, int maxM, int chain);
+/* Force the unchained tile height: bm = 16 or 32, 0 = the rule above (process-global;
+ * SCA_GEMM_LN_BM sets the initial value, read once). */
+int sca_gemm_ln_force_rows(int bm);
 
 /* NN input-gradient GEMM + the backward of the LayerNorm that produced its input, in one
  * launch (d_model = 256).  Per problem:
@@ -537,6 +540,10 @@ int sca_lstm_cell_bwd(const float* dh, const float* dy, const float* act, const 
 
 const char* sca_last_error(void);
 int sca_version(void);
+/* sha256 (first 16 hex digits) of the library sources the binary was built from
+ * (the .cpp, .h and .hip files of scattennet_amd/csrc in name order, then this header); the Python binding
+ * refuses a library whose digest does not match the sources beside it. */
+const char* sca_build_digest(void);
 
 #ifdef __cplusplus
 }

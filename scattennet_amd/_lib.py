@@ -131,6 +131,7 @@ EXPORTS = {
     "sca_gemm_variant": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "sca_gemm_ln_rows": ([c_int, c_int, c_int], c_int),
+    "sca_gemm_ln_force_rows": ([c_int], c_int),
     "sca_gemm_lnb": ([c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_lnb_blocks": ([c_int], c_int),
     "sca_attn_fwd": ([c_int, c_void_p] + [c_int] * 11 + [c_void_p], c_int),
@@ -168,6 +169,7 @@ EXPORTS = {
     "sca_lstm_cell_bwd": ([c_void_p] * 6 + [c_int] * 5 + [c_void_p], c_int),
     "sca_last_error": ([], ctypes.c_char_p),
     "sca_version": ([], c_int),
+    "sca_build_digest": ([], ctypes.c_char_p),
 }
 
 _lib = None
@@ -183,6 +185,13 @@ def lib():
                                "(make -C scattennet_amd/csrc).  There is no fallback path.")
         L = ctypes.CDLL(LIB_PATH)
         alternative = os.environ.get("SCA_LIB_PATH") is not None
+        if not alternative:  # the binary must be the build of the sources beside it
+            built = L.sca_build_digest
+            built.restype = ctypes.c_char_p
+            built = built().decode()
+            if built != library_digest():
+                raise RuntimeError(f"scattennet_amd: {LIB_PATH} was built from other sources (library digest "
+                                   f"{built}, sources {library_digest()}) — rebuild it (make -C scattennet_amd/csrc)")
         for name, (argt, rest) in EXPORTS.items():
             if alternative and not hasattr(L, name):  # an older A/B build: entry points it lacks
                 MISSING.add(name)
@@ -219,6 +228,26 @@ def require_device(*tensors):
         if t is not None and (not t.is_cuda or t.dtype != torch.float32):
             raise RuntimeError("scattennet_amd ops run only on ROCm (MI355X) fp32 tensors; got "
                                f"{t.device} {t.dtype}.  There is no CPU fallback.")
+
+
+def library_digest():
+    """sha256 (first 16 hex digits) of the HIP library's sources: csrc/*.cpp, *.h, *.hip in
+    name order, then include/scatten.h — the same bytes the Makefile hashes into the binary
+    (sca_build_digest)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h")) +
+                   glob.glob(os.path.join(_HERE, "csrc", "*.cpp")), key=os.path.basename)
+    for f in files + [os.path.join(os.path.dirname(_HERE), "include", "scatten.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_digest():
+    """The digest the loaded library was built with."""
+    return lib().sca_build_digest().decode()
 
 
 def source_digest():

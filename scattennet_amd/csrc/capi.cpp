@@ -16,6 +16,12 @@ extern "C" const char* sca_last_error(void) { return g_err; }
 
 extern "C" int sca_version(void) { return 1; }
 
+#ifndef SCA_BUILD_DIGEST
+#error "build through the Makefile: it passes SCA_BUILD_DIGEST (sha256 of the library sources)"
+#endif
+// sha256 (first 16 hex digits) of the sources this library was compiled from (Makefile)
+extern "C" const char* sca_build_digest(void) { return SCA_BUILD_DIGEST; }
+
 namespace {
 const unsigned long long* g_drop_offset = nullptr;
 }

@@ -1977,12 +1977,33 @@ extern "C" int sca_gemm_variant(int layout, int nprob, const sca_gemm_problem* p
 // 32-row tiles (8 waves) whenever they give a workgroup per CU, else 16-row tiles (2
 // workgroups / CU): tools/gemm_ln_bench.py 4x(2048,256,K): K = 768 41.0 vs 44.6 us,
 // K = 256 19.8 vs 20.8 us; 1x(2048,256,256): 15.2 vs 10.9 us.  Chained passes: always 32.
+// A forced tile height (16 / 32; 0 = the rule above): SCA_GEMM_LN_BM, read once on the first
+// launch, or sca_gemm_ln_force_rows (tests that compare launches of different row counts).
+static int g_ln_bm_force = -1;
+
+static int ln_bm_force() {
+  if (g_ln_bm_force < 0) {
+    const char* env = getenv("SCA_GEMM_LN_BM");
+    const int v = env ? atoi(env) : 0;
+    g_ln_bm_force = (v == 16 || v == 32) ? v : 0;
+  }
+  return g_ln_bm_force;
+}
+
+extern "C" int sca_gemm_ln_force_rows(int bm) {
+  if (bm != 0 && bm != 16 && bm != 32) {
+    sca_set_error("sca_gemm_ln_force_rows: bm must be 0, 16 or 32");
+    return SCA_ERR_ARG;
+  }
+  g_ln_bm_force = bm;
+  return SCA_OK;
+}
+
 extern "C" int sca_gemm_ln_rows(int nprob, int maxM, int chain) {
-  const char* env = getenv("SCA_GEMM_LN_BM");  // read per call: tests force one tile height
-  const int bm_env = env ? atoi(env) : 0;
+  const int bm_force = ln_bm_force();
   const long wg32 = (long)nprob * ((maxM + 31) / 32);
   if (chain) return 32;
-  if (bm_env == 16 || bm_env == 32) return bm_env;
+  if (bm_force) return bm_force;
   return wg32 >= 256 ? 32 : 16;
 }
 

@@ -30,6 +30,16 @@ HIP path, the fp32 gradients averaged over all ranks every step (torch.distribut
   backward (or graph replay) all-reduces the flat buffer in place.
 * Averaging: each bucket is pre-scaled by 1/world on the communication stream, then SUM
   all-reduced (exact for power-of-two world sizes).
+* Streams.  Every collective is issued in torch's synchronous form (`async_op=False`), which
+  ProcessGroupNCCL runs on the CURRENT stream (torch >= 2.8; probed on the box by
+  tools/dp_capture_diag.py "watchdog_fixed"), from one of two private communication streams:
+  one for eager steps, one used only while a hipGraph is being captured.  ProcessGroupNCCL's
+  watchdog thread polls the end event of every eager collective until it retires it (every
+  100 ms); hipEventQuery on an event whose stream is capturing at that moment fails with
+  hipErrorCapturedEvent, and the watchdog then terminates the process.  With the eager and
+  the captured collectives on disjoint streams, no event the watchdog can hold is ever on a
+  capturing stream, whatever the timing (the round-4 aborts were this race —
+  the async form put both on the process group's one internal stream).
 
 Oracle: the averaged all-reduced gradient times the world size equals the single-process
 gradient of the whole global batch (sum loss) — tests/test_dp.py checks the reducer with
@@ -66,7 +76,7 @@ class GradBuckets:
         self.slot = {}            # param index -> (offset, numel)
         self.bucket_of = {}       # param index -> bucket index
         self._order, self._count = [], {}
-        self._comm = None
+        self._comms = {}          # False: eager communication stream, True: the capture-only one
         self._step = None
         self.last_fallback = []   # parameter indices reduced by the fallback in the last step
         ops.set_grad_sink(self)
@@ -91,7 +101,7 @@ class GradBuckets:
         fast = self.plan is not None and all(self.params[i].grad is None for i in self.slot)
         self._step = {"fast": fast, "pending": [len(b[2]) for b in self.plan] if fast else None,
                       "streams": [dict() for _ in self.plan] if fast else None, "works": [],
-                      "seen": set(), "producers": {}}
+                      "seen": set(), "producers": {}, "comms": {}}
         torch.autograd.Variable._execution_engine.queue_callback(self._finish)
 
     # ------------------------------------------------------------------ sink protocol (ops)
@@ -137,31 +147,46 @@ class GradBuckets:
         o, n, _ = self.plan[b]
         return self.flat[o:o + n]
 
-    def _comm_stream(self):
-        if self._comm is None:
-            self._comm = torch.cuda.Stream(device=self.params[0].device)
-        return self._comm
+    def _comm_stream(self, capturing):
+        st = self._comms.get(capturing)
+        if st is None:
+            st = self._comms[capturing] = torch.cuda.Stream(device=self.params[0].device)
+        return st
 
-    def _launch(self, b):
-        """Average = pre-scale by 1/world (exact for power-of-two worlds) + SUM all-reduce.
-        The collective is issued from the communication stream (forked from the producers)
-        and waited on by the CALLER's stream at the end of the backward: under hipGraph
-        capture, RCCL's stream may fork from a side stream but must join the capture's
-        origin stream — a wait on it from a forked stream crashes graph instantiation on
-        this ROCm (tools/dp_capture_diag.py: variants "kernel" vs "mainwait")."""
-        if not self.params[0].is_cuda:  # CPU tensors (gloo tests)
-            if self.average:
-                self._bucket(b).mul_(1.0 / self.world)
-            self._step["works"].append(dist.all_reduce(self._bucket(b), async_op=True))
-            return
-        comm = self._comm_stream()
-        for s in self._step["streams"][b].values():
-            comm.wait_stream(s)  # the bucket's gradients are enqueued on these streams
+    def _on_comm(self, waits, body):
+        """Run `body` (which issues collectives in their synchronous form) on a communication
+        stream that first waits on the streams `waits`: the capture-only stream while the
+        current stream is capturing, else the eager one.  Returns the stream; the caller
+        joins it (the caller's stream must wait on it before the gradients are read)."""
+        capturing = torch.cuda.is_current_stream_capturing()
+        comm = self._comm_stream(capturing)
+        for s in waits:
+            comm.wait_stream(s)
             ops.note_fork(comm, s, "RCCL stream")
         with torch.cuda.stream(comm):
+            body()
+        return comm
+
+    def _launch(self, b):
+        """Average = pre-scale by 1/world (exact for power-of-two worlds) + SUM all-reduce,
+        on the communication stream forked from the bucket's producers; the CALLER's stream
+        joins it at the end of the backward (under hipGraph capture a forked stream must join
+        the capture's origin stream directly: a wait on it from another forked stream crashes
+        graph instantiation on this ROCm — tools/dp_capture_diag.py "kernel" vs "mainwait")."""
+        bucket = self._bucket(b)
+        if not self.params[0].is_cuda:  # CPU tensors (gloo tests)
             if self.average:
-                self._bucket(b).mul_(1.0 / self.world)
-            self._step["works"].append(dist.all_reduce(self._bucket(b), async_op=True))
+                bucket.mul_(1.0 / self.world)
+            self._step["works"].append(dist.all_reduce(bucket, async_op=True))
+            return
+
+        def body():
+            if self.average:
+                bucket.mul_(1.0 / self.world)
+            dist.all_reduce(bucket)  # synchronous form: enqueued on the communication stream
+
+        comm = self._on_comm(self._step["streams"][b].values(), body)
+        self._step["comms"][comm.cuda_stream] = comm
 
     def _finish(self):
         st, self._step = self._step, None
@@ -191,9 +216,10 @@ class GradBuckets:
             if p.grad is None or p.grad.data_ptr() != self.flat[o:].data_ptr():
                 p.grad = self.flat[o:o + n].view(p.shape)
         for work in st["works"]:
-            work.wait()  # GPU: the caller's stream waits for RCCL's stream; CPU: completes it
-        if st["works"] and cur is not None:
-            ops.note_join(cur, self._comm_stream())
+            work.wait()  # CPU (gloo) works: completes them
+        for comm in st["comms"].values():  # GPU: the caller's stream joins the RCCL stream
+            cur.wait_stream(comm)
+            ops.note_join(cur, comm)
         self._fallback([i for i, p in enumerate(self.params) if i not in self.slot and p.grad is not None])
 
     def _build_plan(self):
@@ -223,14 +249,29 @@ class GradBuckets:
         if not self.collective or not self.last_fallback:
             return
         grads = [self.params[i].grad for i in self.last_fallback]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat)
-        if self.average:
-            flat.mul_(1.0 / self.world)
-        o = 0
-        for g in grads:
-            g.copy_(flat[o:o + g.numel()].view_as(g))
-            o += g.numel()
+
+        def body():
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat)
+            if self.average:
+                flat.mul_(1.0 / self.world)
+            o = 0
+            for g in grads:
+                g.copy_(flat[o:o + g.numel()].view_as(g))
+                o += g.numel()
+
+        self._collective_here(body)
+
+    def _collective_here(self, body):
+        """`body` ordered on the current stream: on a communication stream (GPU) joined back
+        into the current stream right away; directly (CPU tensors)."""
+        if not self.params[0].is_cuda:
+            body()
+            return
+        cur = torch.cuda.current_stream()
+        comm = self._on_comm([cur], body)
+        cur.wait_stream(comm)
+        ops.note_join(cur, comm)
 
     # ------------------------------------------------------------------ non-overlapped mode
     def sync(self):
@@ -243,20 +284,23 @@ class GradBuckets:
             return
         if self.overlap:
             return
-        dist.all_reduce(self.flat)
-        if self.average:
-            self.flat.mul_(1.0 / self.world)
+
+        def body():
+            dist.all_reduce(self.flat)
+            if self.average:
+                self.flat.mul_(1.0 / self.world)
+
+        self._collective_here(body)
 
     def quiesce(self):
         """Call before capturing a step into a hipGraph: completes every eager kernel and
-        collective of the warm-up.  Capture then runs in `thread_local` mode, in which the
-        calls ProcessGroupNCCL's watchdog thread makes on the warm-up collectives' events
-        (cudaEventQuery from ITS thread) are legal; no collective is issued here (a barrier
-        would be one more eager work for the watchdog to poll), and nothing of the warm-up's
-        autograd graphs may be alive (the caller drops its outputs: a captured backward that
-        reused a warm-up AccumulateGrad node would fork into the warm-up's stream).  The
-        captured collectives themselves are never handed to the watchdog (ProcessGroupNCCL
-        does not track work enqueued while the stream is capturing)."""
+        collective of the warm-up.  Capture runs in `thread_local` mode (ProcessGroupNCCL's
+        watchdog thread queries events from ITS thread while the main thread captures), and
+        nothing of the warm-up's autograd graphs may be alive (the caller drops its outputs: a
+        captured backward that reused a warm-up AccumulateGrad node would fork into the
+        warm-up's stream).  The watchdog may still list warm-up works when capture begins —
+        harmless, because their events sit on the eager communication stream, which is never
+        captured (see the module docstring)."""
         torch.cuda.synchronize()
 
     def bucket_sizes(self):

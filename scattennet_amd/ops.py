@@ -253,6 +253,11 @@ def ln_fusable(N, K):
     return _FUSE_LN and ln_width_ok(N) and K >= 32 and K % 32 == 0
 
 
+def gemm_ln_force_rows(bm):
+    """Force the unchained GEMM + LayerNorm tile height (16 / 32; 0 = the launcher's rule)."""
+    L.check(L.lib().sca_gemm_ln_force_rows(int(bm)), "sca_gemm_ln_force_rows")
+
+
 def gemm_ln(probs, lns, eps):
     """probs: NT sca_gemm problems (C receives the LayerNorm input v); lns: GemmLnProblem."""
     lib = L.lib()
@@ -859,6 +864,11 @@ def sum_tensors(groups):
     if not groups:
         return
     n = groups[0][0].numel()
+    for out, ins in groups:  # the launch applies one n to every problem
+        for t in [out] + list(ins):
+            if t.numel() != n or not t.is_contiguous() or t.dtype != torch.float32 or not t.is_cuda:
+                raise ValueError(f"sum_tensors: every tensor must be a contiguous fp32 GPU tensor of {n} elements; "
+                                 f"got {tuple(t.shape)} {t.dtype} on {t.device}, contiguous={t.is_contiguous()}")
     for c in range(0, len(groups), L.SUM_MAX_PROBLEMS):
         chunk = groups[c:c + L.SUM_MAX_PROBLEMS]
         probs = []
@@ -880,6 +890,7 @@ class FanOut(Function):
     @staticmethod
     def forward(ctx, n, G, *xs):
         ctx.n, ctx.G = n, G
+        ctx.set_materialize_grads(False)  # an alias that got no gradient arrives as None: skipped
         return tuple(x.view_as(x) for _ in range(n) for x in xs)
 
     @staticmethod

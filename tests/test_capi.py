@@ -126,3 +126,29 @@ def test_gemm_variant_ids_are_validated():
         assert lib.sca_gemm_variant(layout, 0, None, 1, None, None, good, None) == OK, (layout, good)
     for layout in range(3):
         assert lib.sca_gemm_tile_override(layout, 0) == OK
+
+
+def test_library_digest_matches_sources():
+    """The loaded binary is the build of the sources beside it: the Makefile embeds the sha256
+    of csrc + include/scatten.h (sca_build_digest) and _lib refuses a mismatch on load."""
+    from scattennet_amd import _lib
+    _lib.lib()
+    assert _lib.build_digest() == _lib.library_digest()
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A binary built from other sources does not load (no silent stale-kernel runs)."""
+    import shutil
+
+    from scattennet_amd import _lib
+    fake_src = tmp_path / "scattennet_amd"
+    shutil.copytree(os.path.join(ROOT, "scattennet_amd", "csrc"), fake_src / "csrc",
+                    ignore=shutil.ignore_patterns("build"))
+    os.makedirs(tmp_path / "include")
+    shutil.copy(os.path.join(ROOT, "include", "scatten.h"), tmp_path / "include" / "scatten.h")
+    with open(fake_src / "csrc" / "common.h", "a") as f:
+        f.write("\n// edited after the build\n")
+    monkeypatch.setattr(_lib, "_HERE", str(fake_src))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        _lib.lib()

@@ -78,7 +78,13 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
     the collective is wrapped so that it DOUBLES its bucket on the communication stream
     before reducing it — every gradient must then come out exactly 2x the plain HIP one, in
     the eager step and in the graph replay (a bucket reduced before its last gradient
-    landed would not be doubled)."""
+    landed would not be doubled).
+
+    The capture also sleeps 0.35 s before it ends: ProcessGroupNCCL's watchdog (100-ms polls)
+    then certainly queries the eager steps' collectives while the captured collectives'
+    stream is capturing — the round-4 SIGABRT (hipErrorCapturedEvent in the watchdog) unless
+    the eager and the captured collectives live on disjoint streams (dp.GradBuckets)."""
+    import time
     import warnings
 
     import torch.distributed as dist
@@ -136,6 +142,7 @@ def test_bucketed_reducer_captured_rccl_world1(monkeypatch):
                 outs = model(kp, mask)
                 torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
                 ops.fork_ledger_end()  # every fork (side streams, branch, RCCL) joined into the origin
+                time.sleep(0.35)  # >= 3 watchdog polls inside the capture
         assert led.last_fork and any("RCCL" in n for n in led.names.values())
         for p in params:  # poison the buckets: the replay must rewrite every planned gradient
             if p.grad is not None:
@@ -166,8 +173,6 @@ def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
     fusion) at B = 64 = 8 shards x 8 clips.  The eight shards' HIP gradients summed equal
     the full 64-clip HIP gradient and the (tie-aware) oracle's full-batch gradient, within
     the north-star 1e-3 — what the 8-GPU all-reduce of config 4 computes."""
-    from scattennet_amd import workloads as W
-    from tests.test_gpu_scale import hip_encoder_step, tie_aware_encoder_oracle
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     # the same kernels for the 8- and the 64-clip launches (the launchers pick 16-row GEMM +
@@ -175,8 +180,17 @@ def test_cfg4_eight_shards_sum_to_full_batch(monkeypatch):
     # compute every clip's forward exactly as the full batch does, so no ReLU / max-pool
     # rounding tie can resolve differently between the two and the sums compare at rounding
     # level
-    monkeypatch.setenv("SCA_GEMM_LN_BM", "32")
     from scattennet_amd import ops
+    ops.gemm_ln_force_rows(32)
+    try:
+        _cfg4_shards(monkeypatch)
+    finally:
+        ops.gemm_ln_force_rows(0)
+
+
+def _cfg4_shards(monkeypatch):
+    from scattennet_amd import ops, workloads as W
+    from tests.test_gpu_scale import hip_encoder_step, tie_aware_encoder_oracle
     monkeypatch.setattr(ops, "_CHAIN_MIN_TILES", 0)  # chained next-op passes at 8 clips too
     dev = torch.device("cuda:0")
     w = dict(W.WORKLOADS["cfg3"], B=64)

@@ -14,7 +14,20 @@ variants (each in its own process; the driver script stops at the first failure)
              waited on the capture stream
   reducer    scattennet_amd.dp.GradBuckets over a small 4-stream SCA step (global capture mode)
   reducer_tl the same with capture_error_mode="thread_local"
+  watchdog_race   (round 5) the round-4 abort, made deterministic: an eager async all_reduce
+             (on ProcessGroupNCCL's internal stream), then at once a thread_local capture that
+             issues an async all_reduce (the same internal stream joins the capture) and sleeps
+             0.5 s inside the capture, so the watchdog's next poll of the eager work's end event
+             falls while that event's stream is capturing.  Expected: hipErrorCapturedEvent
+             from the watchdog thread -> terminate -> SIGABRT.  Run it LAST in a call.
+  watchdog_fixed  the same timing with dp.GradBuckets' stream discipline: eager collectives in
+             the synchronous form on an eager communication stream, the captured one in the
+             synchronous form on a capture-only stream forked from / joined into the origin.
+             Expected: capture, instantiate and replay pass (this also shows that the
+             synchronous form runs on the current stream: on the internal stream it would race
+             exactly like watchdog_race).
 """
+import time
 import os
 import sys
 
@@ -67,9 +80,51 @@ def reducer(variant):
     dist.destroy_process_group()
 
 
+def watchdog(variant):
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29435", rank=0, world_size=1, device_id=dev)
+    x = torch.ones(1 << 20, device=dev)
+    eager_s, cap_s = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    for i in range(3):  # eager works for the watchdog to track; the last one issued just before capture
+        if variant == "watchdog_race":
+            dist.all_reduce(x, async_op=True).wait()
+        else:
+            eager_s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(eager_s):
+                dist.all_reduce(x)
+            torch.cuda.current_stream().wait_stream(eager_s)
+    torch.cuda.synchronize()
+    print("eager collectives done", flush=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        main_s = torch.cuda.current_stream()
+        x.mul_(2.0)
+        if variant == "watchdog_race":
+            dist.all_reduce(x, async_op=True).wait()
+        else:
+            cap_s.wait_stream(main_s)
+            with torch.cuda.stream(cap_s):
+                dist.all_reduce(x)
+            main_s.wait_stream(cap_s)
+        print("  .. collective captured; sleeping inside the capture", flush=True)
+        time.sleep(0.5)  # >= 4 watchdog polls while the collective's stream is capturing
+        x.mul_(0.5)
+    print("captured", flush=True)
+    x.fill_(3.0)
+    g.replay()
+    torch.cuda.synchronize()
+    print("replayed", variant, float(x[0]), "(expect 3.0)", flush=True)
+    time.sleep(0.5)  # let the watchdog poll again after the replay
+    dist.destroy_process_group()
+    print("ok", variant, flush=True)
+
+
 def main(variant):
     if variant.startswith("reducer"):
         return reducer(variant)
+    if variant.startswith("watchdog"):
+        return watchdog(variant)
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29433", rank=0, world_size=1, device_id=dev)
