@@ -28,8 +28,9 @@ HIP path, the fp32 gradients averaged over all ranks every step (torch.distribut
   bench captures forward + backward + the bucketed all-reduces in one hipGraph.
   Without overlap (the `gloo` rehearsal backend, or SCA_DP_OVERLAP=0), `sync()` after the
   backward (or graph replay) all-reduces the flat buffer in place.
-* Averaging: each bucket is pre-scaled by 1/world on the communication stream, then SUM
-  all-reduced (exact for power-of-two world sizes).
+* Averaging: over RCCL one AVG all-reduce per bucket (ncclAvg: the 1/world scale inside the
+  collective, no separate scaling kernel over the 100 MB); over gloo (no AVG) the bucket is
+  pre-scaled by 1/world, then SUM all-reduced (exact for power-of-two world sizes).
 * Streams.  Every collective is issued in torch's synchronous form (`async_op=False`), which
   ProcessGroupNCCL runs on the CURRENT stream (torch >= 2.8; probed on the box by
   tools/dp_capture_diag.py "watchdog_fixed"), from one of two private communication streams:
@@ -168,8 +169,7 @@ class GradBuckets:
         return comm
 
     def _launch(self, b):
-        """Average = pre-scale by 1/world (exact for power-of-two worlds) + SUM all-reduce,
-        on the communication stream forked from the bucket's producers; the CALLER's stream
+        """One AVG (or, unaveraged, SUM) all-reduce of the bucket on the communication stream forked from the bucket's producers; the CALLER's stream
         joins it at the end of the backward (under hipGraph capture a forked stream must join
         the capture's origin stream directly: a wait on it from another forked stream crashes
         graph instantiation on this ROCm — tools/dp_capture_diag.py "kernel" vs "mainwait")."""
@@ -180,10 +180,8 @@ class GradBuckets:
             self._step["works"].append(dist.all_reduce(bucket, async_op=True))
             return
 
-        def body():
-            if self.average:
-                bucket.mul_(1.0 / self.world)
-            dist.all_reduce(bucket)  # synchronous form: enqueued on the communication stream
+        def body():  # synchronous form: enqueued on the communication stream
+            dist.all_reduce(bucket, op=dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM)
 
         comm = self._on_comm(self._step["streams"][b].values(), body)
         self._step["comms"][comm.cuda_stream] = comm
