@@ -35,6 +35,7 @@ struct GemmArgs {
   long slab_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first partial slab in ws
   long bias_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first bias partial row in ws
   unsigned* counters;                           // split-K combined in-launch (sca_gemm_splitk_fused)
+  int nprob;                                    // problems in p[] (the stream-K TN kernel walks them)
 };
 
 // Workgroup tile configuration.
@@ -948,6 +949,301 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 }
 
+// ------------------------------------------------------------------------------ TN, stream-K
+// Weight-gradient GEMM (dW[M x N] = alpha * A^T B over K rows, A = dY [K][M], B = X [K][N],
+// both k-major; bias gradient db = colsum(dY) fused) as a stream-K launch of 8-wave
+// workgroups with NO LDS and NO barrier in the main loop:
+//  * iteration space: every 64x64 output tile of every problem, times its K in blocks of
+//    D 32-k slices; workgroup w (of G, one per CU) walks blocks [w*TB/G, (w+1)*TB/G) — whole
+//    tiles where it covers them, a head / tail piece of a tile where its range starts / ends
+//    inside one.  Every CU gets the same number of slices whatever the tile count (the FFN
+//    shapes have 192 tiles: a split-K grid of 64x64 tiles fills 256 CUs unevenly).
+//  * wave w owns k rows 32s + 4w + g (g = lane >> 4) of every slice s: its lane loads ONE
+//    float4 of A (4 consecutive m) and one of B (4 consecutive n) per slice straight into
+//    registers (coalesced 256-B row pieces), D slices ahead in a register ring, and feeds 16
+//    v_mfma_f32_16x16x4_f32 in outer-product form (MFMA (i, j) takes A's component i and B's
+//    component j: tile rows 4c + i, columns 4c' + j) — each wave accumulates the whole 64x64
+//    tile over its k rows.  No wave reads another wave's operands, so nothing is staged
+//    through LDS and nothing waits on a barrier: 8 independent streams, two per SIMD.
+//  * tile flush: the 8 waves' partial tiles are summed through LDS in fixed wave order (4
+//    passes of 16 rows, 32 KB), giving threads 0..255 one float4 row piece per pass; a tile
+//    covered whole runs the epilogue; a piece is written write-through (sc1) to its
+//    workgroup's slab slot (0: the tile its range starts in, 1: the tile it ends in), drained,
+//    and the workgroup takes a ticket on the tile's counter — the last of the tile's pieces to
+//    arrive sums them in piece (= k) order (its own from registers, in its place) and runs the
+//    epilogue (the G16 recipe of gemm_glds_kernel's in-launch combine; counters left zero).
+//  Deterministic: k order within a lane, lane groups by fixed xor, waves 0..7, pieces in order.
+constexpr int TNS_RED = 8 * 1024 + 8 * 64;  // floats: one 16-row pass of 8 partial tiles + bias rows
+
+// per-problem walk of the stream-K iteration space (blocks of D slices)
+template <int D>
+struct TnsLoc {
+  int p, bx, by, kb, tile;  // problem, tile column / row, block within the tile, global tile index
+  long tb0;                 // first block of the tile
+  int bpt;                  // blocks per tile
+};
+
+template <int D>
+__device__ __forceinline__ TnsLoc<D> tns_locate(const GemmArgs& a, long b) {
+  TnsLoc<D> L{0, 0, 0, 0, 0, 0, 1};
+  long off = 0;
+  int tbase = 0;
+  for (int p = 0; p < a.nprob; ++p) {
+    const sca_gemm_problem& P = a.p[p];
+    const int tn = (P.N + 63) >> 6, tm = (P.M + 63) >> 6, bpt = P.seg[0].K / (32 * D);
+    const long n = (long)tm * tn * bpt;
+    if (b < off + n || p == a.nprob - 1) {
+      const long r = b - off;
+      const int tile = (int)(r / bpt);
+      L.p = p;
+      L.kb = (int)(r - (long)tile * bpt);
+      L.by = tile / tn;
+      L.bx = tile - L.by * tn;
+      L.tile = tbase + tile;
+      L.tb0 = b - L.kb;
+      L.bpt = bpt;
+      return L;
+    }
+    off += n;
+    tbase += tm * tn;
+  }
+  return L;
+}
+
+// byte offset of a __shared__ location (the address operand of an inline-asm ds_read)
+__device__ __forceinline__ unsigned lds_off(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int D>
+__device__ __forceinline__ long tns_blocks(const GemmArgs& a) {
+  long tb = 0;
+  for (int p = 0; p < a.nprob; ++p) {
+    const sca_gemm_problem& P = a.p[p];
+    tb += (long)((P.M + 63) >> 6) * ((P.N + 63) >> 6) * (P.seg[0].K / (32 * D));
+  }
+  return tb;
+}
+
+
+template <int D, int S>
+__global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(16))) float red[TNS_RED];
+  __shared__ __attribute__((aligned(1024))) char ring[8 * S * 2048];
+  __shared__ unsigned flag;
+  const int G = (int)gridDim.x;
+  const unsigned orig = blockIdx.x, xcd = orig & 7, q8 = (unsigned)G >> 3, r8 = (unsigned)G & 7;
+  const int w = (int)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3));
+  const long TB = tns_blocks<D>(args);
+  const long b0 = (long)w * TB / G, b1 = (long)(w + 1) * TB / G;
+  if (b0 >= b1) return;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int t = threadIdx.x;  // < 256: this thread's float4 of a flush pass (rows 16tg + 4r + ti, cols 4tc)
+  const int tg = t >> 6, ti = (t >> 4) & 3, tc = t & 15;
+
+  // load cursor: the block / slice being loaded next, and this lane's operand pointers at
+  // that block's first slice (a slice is 32 k rows further)
+  long lb = b0;
+  int lj = 0;
+  const float *pa = nullptr, *pb = nullptr;
+  long sa = 0, sb = 0;
+  auto ptrs = [&](long blk) {
+    const TnsLoc<D> L = tns_locate<D>(args, blk);
+    const sca_gemm_problem& P = args.p[L.p];
+    const sca_gemm_seg& Sg = P.seg[0];
+    const long k = (long)L.kb * (32 * D) + 4 * wave + g;
+    pa = Sg.A + k * Sg.lda + min(L.by * 64 + 4 * c, P.M - 4);
+    pb = Sg.B + k * Sg.ldb + min(L.bx * 64 + 4 * c, P.N - 4);
+    sa = 32L * Sg.lda;
+    sb = 32L * Sg.ldb;
+  };
+  ptrs(b0);
+  // this wave's private LDS ring: stage = A piece (4 k rows x 64 m) + B piece (4 x 64 n),
+  // written by the wave's own two DMA instructions, read back lane-for-lane (each lane reads
+  // the 16 bytes it loaded itself) — so no barrier, and the waits are explicit vmcnt counts
+  char* wring = ring + wave * (S * 2048);
+  auto issue = [&](int stage) {
+    char* dst = wring + stage * 2048;
+    gl_dma(pa + lj * sa, dst);
+    gl_dma(pb + lj * sb, dst + 1024);
+    if (++lj == D) {
+      if (lb + 1 < b1) {
+        lj = 0;
+        ptrs(++lb);
+      } else {
+        lj = D - 1;  // past the range: reload the last slice (never read; keeps the counts uniform)
+      }
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i) issue(i);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
+  TnsLoc<D> cur = tns_locate<D>(args, b0);
+  int stage = 0;  // stage of the slice computed next
+
+  for (long b = b0; b < b1; ++b) {
+    const bool do_bias = args.p[cur.p].bias_grad != nullptr && cur.bx == 0;
+    for (int j = 0; j < D; ++j) {
+      gl_wait_vm<2 * (S - 2)>();  // this slice's two pieces landed (S - 2 younger slices may fly)
+      // the read-back as inline asm: the compiler would guard a plain LDS load with vmcnt(0)
+      // (it cannot tell the load from the ring's in-flight DMA destinations)
+      f32x4 a, bb;
+      const unsigned src = lds_off(wring + stage * 2048 + 16 * lane);
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(a), "=&v"(bb)
+                   : "v"(src));
+      issue(stage == 0 ? S - 1 : stage - 1);  // the stage read by the previous slice
+      stage = stage == S - 1 ? 0 : stage + 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma16(a[i], bb[jj], acc[i][jj]);
+      if (do_bias) bs4 += a;
+    }
+    const bool tile_end = b + 1 == b1 || b + 1 - cur.tb0 == cur.bpt;
+    if (!tile_end) {
+      if (b + 1 < b1) cur = tns_locate<D>(args, b + 1);
+      continue;
+    }
+
+    // ---- flush the tile (or this workgroup's piece of it)
+    const sca_gemm_problem& P = args.p[cur.p];
+    const int m0 = cur.by * 64, n0 = cur.bx * 64;
+    float* bred = red + 8 * 1024;
+    if (do_bias) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bs4[q] += __shfl_xor(bs4[q], 16, 64);
+        bs4[q] += __shfl_xor(bs4[q], 32, 64);
+      }
+    }
+    f32x4 sum[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      lds_barrier();  // the previous pass's (or flush's) reads are done
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        st4(red + wave * 1024 + ((g * 4 + i) * 16 + c) * 4,
+            f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]});
+      if (r == 0 && do_bias && g == 0) st4(bred + wave * 64 + 4 * c, bs4);
+      lds_barrier();
+      if (t < 256) {
+        f32x4 s4 = ld4(red + 4 * t);
+#pragma unroll
+        for (int ww = 1; ww < 8; ++ww) s4 += ld4(red + ww * 1024 + 4 * t);
+        sum[r] = s4;
+      }
+    }
+    float bsum = 0.f;
+    if (do_bias && t < 64) {
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) bsum += bred[ww * 64 + t];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bs4 = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const long tb1 = cur.tb0 + cur.bpt;
+    const int wa = (int)(((cur.tb0 + 1) * G - 1) / TB), wb = (int)((tb1 * G - 1) / TB);
+    const float alpha = P.seg[0].alpha;
+    bool finish = wa == wb;  // the whole tile was this workgroup's
+    if (!finish) {
+      // write this piece (slot 0 if the tile is the one this workgroup's range starts in)
+      const int slot = b0 >= cur.tb0 ? 0 : 1;
+      float* slab = args.ws + (long)(2 * w + slot) * 4096;
+      float* bslab = args.ws + (long)G * 2 * 4096 + (long)(2 * w + slot) * 64;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, 4096 * 4, 0x00020000);
+      if (t < 256) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const f32x4 x = sum[r];
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs,
+                                                 ((16 * tg + 4 * r + ti) * 64 + 4 * tc) * 4, 0, 16);
+        }
+      }
+      if (do_bias && t < 64) __hip_atomic_store(bslab + t, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+      __syncthreads();
+      unsigned* cnt = args.counters + cur.tile;
+      if (t == 0)
+        flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(wb - wa);
+      __syncthreads();
+      finish = flag != 0;
+      if (finish) {
+        if (t == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded
+        f32x4 tot[4];
+        float btot = 0.f;
+        for (int wq = wa; wq <= wb; ++wq) {  // pieces in k order
+          const long q0 = (long)wq * TB / G;
+          const int sq = q0 >= cur.tb0 ? 0 : 1;
+          const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+              args.ws + (long)(2 * wq + sq) * 4096, 0, 4096 * 4, 0x00020000);
+          const float* bq = args.ws + (long)G * 2 * 4096 + (long)(2 * wq + sq) * 64;
+          if (t < 256) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const f32x4 x = wq == w ? sum[r] : ld4_sc1(rq, (16 * tg + 4 * r + ti) * 64 + 4 * tc);
+              tot[r] = wq == wa ? x : tot[r] + x;
+            }
+          }
+          if (do_bias && t < 64) {
+            const float x = wq == w ? bsum : __hip_atomic_load(bq + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            btot = wq == wa ? x : btot + x;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum[r] = tot[r];
+        bsum = btot;
+      }
+    }
+    if (finish) {
+      if (do_bias && t < 64 && m0 + t < P.M) P.bias_grad[m0 + t] = bsum * alpha * P.bias_grad_scale;
+      if (t < 256) {
+        const int n = n0 + 4 * tc;
+        DropMask dm;
+        if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + 16 * tg + 4 * r + ti;
+          if (m >= P.M || n >= P.N) continue;
+          f32x4 o = (sum[r] * alpha + (P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f})) * P.post_scale;
+          if (P.epi & SCA_EPI_GELU) {
+            st4(P.aux_out + (long)m * P.ldo + n, o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
+          }
+          if (P.epi & SCA_EPI_DROPOUT) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), o[j]);
+          }
+          if (P.epi & SCA_EPI_DGELU) {
+            const f32x4 ax = ld4(P.aux + (long)m * P.ldx + n);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
+          }
+          f32x4 ex = {0.f, 0.f, 0.f, 0.f};
+          if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
+          if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
+          st4(P.C + (long)m * P.ldc + n, o + ex);
+        }
+      }
+    }
+    gl_wait_vm<0>();  // the flush's own memory operations shifted the ring's counts
+    if (b + 1 < b1) cur = tns_locate<D>(args, b + 1);
+  }
+}
+
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -1774,6 +2070,30 @@ int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
+template <int D>
+int launch_tns(const GemmArgs& a, int nwg, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_tns_kernel<D, 4>), dim3(nwg), dim3(512), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
+// the stream-K TN kernel's shape requirements (float4 operand loads and row stores, whole
+// blocks of D 32-k slices)
+bool tns_ok(const sca_gemm_problem* probs, int nprob, int D) {
+  for (int i = 0; i < nprob; ++i) {
+    const sca_gemm_problem& P = probs[i];
+    const sca_gemm_seg& S = P.seg[0];
+    if (P.nseg != 1 || P.M < 4 || P.N < 4 || (P.M & 3) || (P.N & 3) || S.K <= 0 || (S.K % (32 * D)) || !S.A ||
+        !S.B || !P.C || (S.lda & 3) || (S.ldb & 3) || (P.ldc & 3) || S.lda < P.M || S.ldb < P.N || P.ldc < P.N ||
+        ((reinterpret_cast<uintptr_t>(S.A) | reinterpret_cast<uintptr_t>(S.B) | reinterpret_cast<uintptr_t>(P.C)) & 15) ||
+        (P.resid && ((P.ldr & 3) || (reinterpret_cast<uintptr_t>(P.resid) & 15))) ||
+        (P.bias && (reinterpret_cast<uintptr_t>(P.bias) & 15)) ||
+        ((P.epi & SCA_EPI_GELU) && ((P.ldo & 3) || (reinterpret_cast<uintptr_t>(P.aux_out) & 15))) ||
+        ((P.epi & SCA_EPI_DGELU) && ((P.ldx & 3) || (reinterpret_cast<uintptr_t>(P.aux) & 15))))
+      return false;
+  }
+  return true;
+}
+
 bool tn_ok(const GemmArgs& a, int nprob) {
   for (int i = 0; i < nprob; ++i)
     if (a.p[i].nseg != 1) return false;
@@ -1851,6 +2171,7 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   }
   GemmArgs a;
   a.splitk = splitk;
+  a.nprob = nprob;
   a.ws = workspace;
   a.drop_off = sca_drop_offset_ptr();
   a.counters = nullptr;
@@ -1954,6 +2275,65 @@ extern "C" int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* p
 extern "C" int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                                void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, false, true);
+}
+
+namespace {
+int g_cu_count = 0;
+int cu_count() {
+  if (!g_cu_count) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      g_cu_count = n;
+    if (g_cu_count <= 0) g_cu_count = 256;
+  }
+  return g_cu_count;
+}
+}  // namespace
+
+extern "C" long sca_gemm_tn_streamk_workspace(int nwg) {
+  if (nwg <= 0) nwg = cu_count();
+  return (long)nwg * 2 * (4096 + 64);
+}
+
+extern "C" long sca_gemm_tn_streamk_tiles(int nprob, const sca_gemm_problem* probs) {
+  long n = 0;
+  for (int i = 0; i < nprob; ++i) n += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
+  return n;
+}
+
+extern "C" int sca_gemm_tn_streamk(int nprob, const sca_gemm_problem* probs, int nwg, int slices_per_block,
+                                   float* workspace, unsigned* counters, void* stream) {
+  if (nprob <= 0) return SCA_OK;
+  if (nprob > SCA_GEMM_MAX_PROBLEMS || !probs || !workspace || !counters ||
+      (slices_per_block != 0 && slices_per_block != 4 && slices_per_block != 8)) {
+    sca_set_error("sca_gemm_tn_streamk: bad nprob / pointers / slices_per_block");
+    return SCA_ERR_ARG;
+  }
+  int D = slices_per_block;
+  if (!D) D = tns_ok(probs, nprob, 8) ? 8 : 4;
+  if (!tns_ok(probs, nprob, D)) {
+    sca_set_error("sca_gemm_tn_streamk: needs one segment per problem, K a positive multiple of 32 x the "
+                  "slices per block, M, N >= 4 and M, N, lda, ldb, ldc multiples of 4, 16-byte aligned operands");
+    return SCA_ERR_ARG;
+  }
+  if (nwg <= 0) nwg = cu_count();
+  GemmArgs a;
+  a.splitk = 1;
+  a.ws = workspace;
+  a.counters = counters;
+  a.drop_off = sca_drop_offset_ptr();
+  a.nprob = nprob;
+  long tb = 0;
+  for (int i = 0; i < nprob; ++i) {
+    a.p[i] = probs[i];
+    tb += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64) * (probs[i].seg[0].K / (32 * D));
+  }
+  if (tb == 0) return SCA_OK;
+  if (nwg > tb) nwg = (int)tb;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int rc = D == 8 ? launch_tns<8>(a, nwg, st) : launch_tns<4>(a, nwg, st);
+  if (rc != SCA_OK) sca_set_error("sca_gemm_tn_streamk: launch failed");
+  return rc;
 }
 
 extern "C" long sca_gemm_splitk_counters(int nprob, int maxM, int maxN) {

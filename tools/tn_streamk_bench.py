@@ -1,0 +1,98 @@
+"""Weight-gradient GEMM shapes of configs 2 / 5: the stream-K kernel (sca_gemm_tn_streamk) against
+the k-split kernel (tile 36, the round-4 default) and the library (torch.bmm -> hipBLASLt), each
+checked against float64 first, timed as graph replays of 20 launches, best of 3 rounds.
+
+    python tools/tn_streamk_bench.py [--iters 20] [--rounds 3]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from scattennet_amd import _lib as L, ops  # noqa: E402
+
+PEAK = 157.3
+
+
+def case(name, shapes, K):
+    items = []
+    for (M, N) in shapes:
+        dY, X = torch.randn(K, M, device="cuda"), torch.randn(K, N, device="cuda")
+        items.append((dY, X, torch.empty(M, N, device="cuda"), torch.empty(M, device="cuda")))
+    return dict(name=name, items=items, flops=sum(2.0 * K * M * N for M, N in shapes), K=K)
+
+
+def probs(c):
+    return [ops._prob([ops._seg(dY, X, dW.shape[0], dW.shape[1], c["K"])], dW, dW.shape[0], dW.shape[1], dW.shape[1],
+                      bias_grad=db) for dY, X, dW, db in c["items"]]
+
+
+def variants(c):
+    P = probs(c)
+    out = []
+    for nwg in (256, 128):
+        for spb in (4, 8):
+            out.append((f"streamK nwg={nwg} spb={spb}", lambda nwg=nwg, spb=spb: ops.gemm_tn_streamk(P, nwg, spb)))
+    tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
+    for sk in (2, 3):
+        ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
+        out.append((f"ksplit36 sk={sk} wg={tiles * sk}", lambda sk=sk, ws=ws: ops.gemm(L.GEMM_TN, P, splitk=sk, ws=ws,
+                                                                                       tile=36)))
+    if len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
+        A = torch.stack([dY for dY, _, _, _ in c["items"]])
+        B = torch.stack([X for _, X, _, _ in c["items"]])
+        out.append(("hipBLASLt bmm (no bias)", lambda: torch.bmm(A.transpose(1, 2), B)))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    cases = [case("cfg2 attn 16x(256,256)", [(256, 256)] * 16, 2048),
+             case("cfg2 fc1 4x(768,256)", [(768, 256)] * 4, 2048),
+             case("cfg2 fc2 4x(256,768)", [(256, 768)] * 4, 2048),
+             case("cfg5 attn 16x(512,512)", [(512, 512)] * 16, 8192),
+             case("cfg5 fc1 4x(1536,512)", [(1536, 512)] * 4, 8192)]
+    runs = []
+    for c in cases:
+        ref = [(dY.double().t() @ X.double(), dY.double().sum(0)) for dY, X, _, _ in c["items"]]
+        for name, fn in variants(c):
+            for _, _, dW, db in c["items"]:
+                dW.fill_(float("nan"))
+                db.fill_(float("nan"))
+            fn()
+            torch.cuda.synchronize()
+            if "bmm" not in name:
+                for (_, _, dW, db), (rw, rb) in zip(c["items"], ref):
+                    ew = float((dW.double() - rw).abs().max() / rw.abs().max())
+                    eb = float((db.double() - rb).abs().max() / rb.abs().max())
+                    assert ew < 2e-5 and eb < 2e-5, (c["name"], name, ew, eb)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(args.iters):
+                    fn()
+            runs.append((c, name, g))
+    best = {}
+    for _ in range(args.rounds):
+        for c, name, g in runs:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            k = (c["name"], name)
+            best[k] = min(best.get(k, 1e30), us)
+    for c, name, _ in runs:
+        us = best[(c["name"], name)]
+        tf = c["flops"] / us / 1e6
+        print(f"{c['name']:24s} {name:28s} {us:8.2f} us {tf:7.1f} TFLOP/s ({tf / PEAK:.3f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
