@@ -149,3 +149,30 @@ def test_ksplit_tile_falls_back_when_k_is_ragged():
     ops.gemm(L.GEMM_TN, _probs(items), splitk=1, tile=36)
     torch.cuda.synchronize()
     _check(items)
+
+
+@pytest.mark.gpu
+def test_streamk_in_captured_graph():
+    """Captured (as in the bench step) and replayed: several launches back to back on fresh
+    workspace from the graph pool and counters from the ring, replayed twice."""
+    from scattennet_amd import ops
+    items = _case([(256, 256)] * 4 + [(768, 256)], 2048, seed=12)
+    items2 = _case([(256, 768)] * 2, 1024, seed=13)
+    p1, p2 = _probs(items), _probs(items2, alpha=0.5)
+    ops.gemm_tn_streamk(p1)  # warm (lazy state) outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(3):
+            ops.gemm_tn_streamk(p1)
+            ops.gemm_tn_streamk(p2, nwg=37)
+    for _, _, dW, db in items + items2:
+        dW.fill_(float("nan"))
+        db.fill_(float("nan"))
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    _check(items)
+    _check(items2, alpha=0.5)
+    for ring, _ in ops._CNT.values():
+        assert int(ring.abs().sum()) == 0

@@ -43,7 +43,8 @@ def variants(c):
     if len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
         A = torch.stack([dY for dY, _, _, _ in c["items"]])
         B = torch.stack([X for _, X, _, _ in c["items"]])
-        out.append(("hipBLASLt bmm (no bias)", lambda: torch.bmm(A.transpose(1, 2), B)))
+        C = torch.empty(len(c["items"]), A.shape[2], B.shape[2], device="cuda")
+        out.append(("hipBLASLt bmm (no bias)", lambda: torch.bmm(A.transpose(1, 2), B, out=C)))
     return out
 
 
@@ -59,7 +60,9 @@ def main():
              case("cfg5 attn 16x(512,512)", [(512, 512)] * 16, 8192),
              case("cfg5 fc1 4x(1536,512)", [(1536, 512)] * 4, 8192)]
     runs = []
+    print("checking + capturing", flush=True)
     for c in cases:
+        print(" ", c["name"], flush=True)
         ref = [(dY.double().t() @ X.double(), dY.double().sum(0)) for dY, X, _, _ in c["items"]]
         for name, fn in variants(c):
             for _, _, dW, db in c["items"]:
@@ -72,17 +75,31 @@ def main():
                     ew = float((dW.double() - rw).abs().max() / rw.abs().max())
                     eb = float((db.double() - rb).abs().max() / rb.abs().max())
                     assert ew < 2e-5 and eb < 2e-5, (c["name"], name, ew, eb)
+            for ring, _ in ops._CNT.values():  # every tile counter back at zero
+                assert int(ring.abs().sum()) == 0, (c["name"], name, "tile counters left non-zero")
+            if "bmm" in name:  # the library eagerly (not captured): launches back to back
+                runs.append((c, name, fn))
+                continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(args.iters):
                     fn()
             runs.append((c, name, g))
     best = {}
+    print("timing", flush=True)
+    for c, name, g in runs:  # one checked replay each first: a fault names its variant
+        print(" ", c["name"], name, flush=True)
+        g.replay() if isinstance(g, torch.cuda.CUDAGraph) else g()
+        torch.cuda.synchronize()
     for _ in range(args.rounds):
         for c, name, g in runs:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            g.replay()
+            if isinstance(g, torch.cuda.CUDAGraph):
+                g.replay()
+            else:
+                for _ in range(args.iters):
+                    g()
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / args.iters
