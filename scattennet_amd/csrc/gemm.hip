@@ -952,67 +952,79 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
 // ------------------------------------------------------------------------------ TN, stream-K
 // Weight-gradient GEMM (dW[M x N] = alpha * A^T B over K rows, A = dY [K][M], B = X [K][N],
 // both k-major; bias gradient db = colsum(dY) fused) as a stream-K launch of 8-wave
-// workgroups with NO LDS and NO barrier in the main loop:
-//  * iteration space: every 64x64 output tile of every problem, times its K in blocks of
-//    D 32-k slices; workgroup w (of G, one per CU) walks blocks [w*TB/G, (w+1)*TB/G) — whole
-//    tiles where it covers them, a head / tail piece of a tile where its range starts / ends
-//    inside one.  Every CU gets the same number of slices whatever the tile count (the FFN
-//    shapes have 192 tiles: a split-K grid of 64x64 tiles fills 256 CUs unevenly).
-//  * wave w owns k rows 32s + 4w + g (g = lane >> 4) of every slice s: its lane loads ONE
-//    float4 of A (4 consecutive m) and one of B (4 consecutive n) per slice straight into
-//    registers (coalesced 256-B row pieces), D slices ahead in a register ring, and feeds 16
-//    v_mfma_f32_16x16x4_f32 in outer-product form (MFMA (i, j) takes A's component i and B's
-//    component j: tile rows 4c + i, columns 4c' + j) — each wave accumulates the whole 64x64
-//    tile over its k rows.  No wave reads another wave's operands, so nothing is staged
-//    through LDS and nothing waits on a barrier: 8 independent streams, two per SIMD.
-//  * tile flush: the 8 waves' partial tiles are summed through LDS in fixed wave order (4
-//    passes of 16 rows, 32 KB), giving threads 0..255 one float4 row piece per pass; a tile
-//    covered whole runs the epilogue; a piece is written write-through (sc1) to its
-//    workgroup's slab slot (0: the tile its range starts in, 1: the tile it ends in), drained,
-//    and the workgroup takes a ticket on the tile's counter — the last of the tile's pieces to
-//    arrive sums them in piece (= k) order (its own from registers, in its place) and runs the
-//    epilogue (the G16 recipe of gemm_glds_kernel's in-launch combine; counters left zero).
-//  Deterministic: k order within a lane, lane groups by fixed xor, waves 0..7, pieces in order.
-constexpr int TNS_RED = 8 * 1024 + 8 * 64;  // floats: one 16-row pass of 8 partial tiles + bias rows
+// workgroups over 128x128 output tiles:
+//  * iteration space: every 128x128 tile of every problem, times its K in blocks of D 32-k
+//    slices; workgroup w (of G, one per CU) walks blocks [w*TB/G, (w+1)*TB/G) — whole tiles
+//    where it covers them, a head / tail piece of a tile where its range starts / ends
+//    inside one.  Every CU gets the same number of slices whatever the tile count.
+//  * 128x128 tiles halve the operand bytes per FLOP of a 64x64 tile: 8 B per clock per CU at
+//    the fp32 MFMA rate (1 KB per k row for 32K FLOP), against ~18 B per clock the LDS-DMA
+//    path delivers per CU (a 64x64 tile needs 16: measured, its DMA alone took 60 % of its
+//    MFMA time).  Operands go through a 3-stage LDS-DMA ring (k-major images [32 k][128],
+//    32 KB per slice, one barrier per slice).
+//  * wave (wm, wn) = (wave >> 2, wave & 3) owns rows 64 wm .. +63 and columns 32 wn .. +31.
+//    Per k-step (4 k, lane group g = lane >> 4 takes k = 4s + g) a lane reads ONE float4 of A
+//    (m = 64 wm + 4c + i) and one float2 of B (n = 32 wn + 2c + j) and feeds 8
+//    v_mfma_f32_16x16x4_f32 in outer-product form (MFMA (i, j): A component i, B component j),
+//    so a lane ends with rows 64 wm + 16g + 4r + i x columns 32 wn + 2c + j.
+//  * a tile's pieces: written write-through (sc1) to the workgroup's slab slot (0: the tile its
+//    range starts in, 1: the tile it ends in), drained, then a ticket on the tile's counter —
+//    the last piece to arrive sums them in piece (= k) order, its own from registers in its
+//    place, and runs the epilogue (the G16 recipe of the in-launch split-K combine; counters
+//    left zero).  Deterministic: k order within a lane, pieces in order.
+constexpr int TNW_T = 128;                  // tile edge
+constexpr int TNW_SLICE = 2 * 32 * TNW_T * 4;  // bytes per 32-k slice (A + B images)
+constexpr int TNW_SLAB = TNW_T * TNW_T;     // floats per slab slot
 
-// per-problem walk of the stream-K iteration space (blocks of D slices)
-template <int D>
-struct TnsLoc {
-  int p, bx, by, kb, tile;  // problem, tile column / row, block within the tile, global tile index
-  long tb0;                 // first block of the tile
-  int bpt;                  // blocks per tile
+// The stream-K iteration space, walked incrementally: problem p, tile row by / column bx
+// (tiles of a problem in row-major order), block kb of the tile's bpt blocks of D slices;
+// `tile` = the tile's index over all problems (its counter).  Only the workgroup's first
+// block is located by search; after that a block step is a few compares.
+struct TnsCur {
+  int p, by, bx, kb, tile;
+  int tm, tn, bpt;
 };
 
 template <int D>
-__device__ __forceinline__ TnsLoc<D> tns_locate(const GemmArgs& a, long b) {
-  TnsLoc<D> L{0, 0, 0, 0, 0, 0, 1};
-  long off = 0;
-  int tbase = 0;
-  for (int p = 0; p < a.nprob; ++p) {
-    const sca_gemm_problem& P = a.p[p];
-    const int tn = (P.N + 63) >> 6, tm = (P.M + 63) >> 6, bpt = P.seg[0].K / (32 * D);
-    const long n = (long)tm * tn * bpt;
-    if (b < off + n || p == a.nprob - 1) {
-      const long r = b - off;
-      const int tile = (int)(r / bpt);
-      L.p = p;
-      L.kb = (int)(r - (long)tile * bpt);
-      L.by = tile / tn;
-      L.bx = tile - L.by * tn;
-      L.tile = tbase + tile;
-      L.tb0 = b - L.kb;
-      L.bpt = bpt;
-      return L;
-    }
-    off += n;
-    tbase += tm * tn;
-  }
-  return L;
+__device__ __forceinline__ void tns_shape(const GemmArgs& a, TnsCur& c) {
+  const sca_gemm_problem& P = a.p[c.p];
+  c.tm = (P.M + TNW_T - 1) / TNW_T;
+  c.tn = (P.N + TNW_T - 1) / TNW_T;
+  c.bpt = P.seg[0].K / (32 * D);
 }
 
-// byte offset of a __shared__ location (the address operand of an inline-asm ds_read)
-__device__ __forceinline__ unsigned lds_off(const char* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+template <int D>
+__device__ __forceinline__ TnsCur tns_locate(const GemmArgs& a, long b) {
+  TnsCur c{0, 0, 0, 0, 0, 1, 1, 1};
+  int tbase = 0;
+  for (c.p = 0; c.p < a.nprob; ++c.p) {
+    tns_shape<D>(a, c);
+    const long n = (long)c.tm * c.tn * c.bpt;
+    if (b < n || c.p == a.nprob - 1) break;
+    b -= n;
+    tbase += c.tm * c.tn;
+  }
+  const int tile = (int)(b / c.bpt);
+  c.kb = (int)(b - (long)tile * c.bpt);
+  c.by = tile / c.tn;
+  c.bx = tile - c.by * c.tn;
+  c.tile = tbase + tile;
+  return c;
+}
+
+// next block; returns true when it starts a new tile
+template <int D>
+__device__ __forceinline__ bool tns_step(const GemmArgs& a, TnsCur& c) {
+  if (++c.kb < c.bpt) return false;
+  c.kb = 0;
+  ++c.tile;
+  if (++c.bx < c.tn) return true;
+  c.bx = 0;
+  if (++c.by < c.tm) return true;
+  c.by = 0;
+  ++c.p;
+  if (c.p < a.nprob) tns_shape<D>(a, c);
+  return true;
 }
 
 template <int D>
@@ -1020,16 +1032,22 @@ __device__ __forceinline__ long tns_blocks(const GemmArgs& a) {
   long tb = 0;
   for (int p = 0; p < a.nprob; ++p) {
     const sca_gemm_problem& P = a.p[p];
-    tb += (long)((P.M + 63) >> 6) * ((P.N + 63) >> 6) * (P.seg[0].K / (32 * D));
+    tb += (long)((P.M + TNW_T - 1) / TNW_T) * ((P.N + TNW_T - 1) / TNW_T) * (P.seg[0].K / (32 * D));
   }
   return tb;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// byte offset of a __shared__ location (the address operand of an inline-asm ds_read)
+__device__ __forceinline__ unsigned lds_off(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
 
 template <int D, int S>
 __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(16))) float red[TNS_RED];
-  __shared__ __attribute__((aligned(1024))) char ring[8 * S * 2048];
+  __shared__ __attribute__((aligned(1024))) char ring[S * TNW_SLICE];
+  __shared__ float bred[2][4][64];  // bias partials: [wm][g][64 rows]
   __shared__ unsigned flag;
   const int G = (int)gridDim.x;
   const unsigned orig = blockIdx.x, xcd = orig & 7, q8 = (unsigned)G >> 3, r8 = (unsigned)G & 7;
@@ -1040,207 +1058,223 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int t = threadIdx.x;  // < 256: this thread's float4 of a flush pass (rows 16tg + 4r + ti, cols 4tc)
-  const int tg = t >> 6, ti = (t >> 4) & 3, tc = t & 15;
+  const int wm = wave >> 2, wn = wave & 3;
 
-  // load cursor: the block / slice being loaded next, and this lane's operand pointers at
-  // that block's first slice (a slice is 32 k rows further)
-  long lb = b0;
+  // load cursor: the slice loaded next and this lane's DMA sources in it (wave w loads image
+  // rows 4w .. 4w+3 of A and of B: pieces q = 0, 1 of two k rows each; lane -> row lane >> 5,
+  // columns 4 (lane & 31) .. +3); within a tile consecutive blocks are consecutive k, so the
+  // pointers just advance by a slice — recomputed only when a new tile starts
+  TnsCur lc = tns_locate<D>(args, b0);
+  long lrem = b1 - b0;
   int lj = 0;
-  const float *pa = nullptr, *pb = nullptr;
-  long sa = 0, sb = 0;
-  auto ptrs = [&](long blk) {
-    const TnsLoc<D> L = tns_locate<D>(args, blk);
-    const sca_gemm_problem& P = args.p[L.p];
+  const float *pa, *pb;
+  long sa, sb;
+  auto ptrs = [&]() {
+    const sca_gemm_problem& P = args.p[lc.p];
     const sca_gemm_seg& Sg = P.seg[0];
-    const long k = (long)L.kb * (32 * D) + 4 * wave + g;
-    pa = Sg.A + k * Sg.lda + min(L.by * 64 + 4 * c, P.M - 4);
-    pb = Sg.B + k * Sg.ldb + min(L.bx * 64 + 4 * c, P.N - 4);
+    const long k = (long)lc.kb * (32 * D) + 4 * wave + (lane >> 5);
+    pa = Sg.A + k * Sg.lda + min(lc.by * TNW_T + 4 * (lane & 31), P.M - 4);
+    pb = Sg.B + k * Sg.ldb + min(lc.bx * TNW_T + 4 * (lane & 31), P.N - 4);
     sa = 32L * Sg.lda;
     sb = 32L * Sg.ldb;
   };
-  ptrs(b0);
-  // this wave's private LDS ring: stage = A piece (4 k rows x 64 m) + B piece (4 x 64 n),
-  // written by the wave's own two DMA instructions, read back lane-for-lane (each lane reads
-  // the 16 bytes it loaded itself) — so no barrier, and the waits are explicit vmcnt counts
-  char* wring = ring + wave * (S * 2048);
+  ptrs();
   auto issue = [&](int stage) {
-    char* dst = wring + stage * 2048;
-    gl_dma(pa + lj * sa, dst);
-    gl_dma(pb + lj * sb, dst + 1024);
-    if (++lj == D) {
-      if (lb + 1 < b1) {
-        lj = 0;
-        ptrs(++lb);
+    char* dst = ring + stage * TNW_SLICE + wave * 2048;  // image rows 4w .. 4w+3 (512 B each)
+    gl_dma(pa, dst);
+    gl_dma(pa + 2 * (sa >> 5), dst + 1024);
+    gl_dma(pb, dst + 16384);
+    gl_dma(pb + 2 * (sb >> 5), dst + 16384 + 1024);
+    if (++lj < D) {
+      pa += sa;
+      pb += sb;
+    } else if (lrem > 1) {  // next block
+      lj = 0;
+      --lrem;
+      if (tns_step<D>(args, lc)) {
+        ptrs();
       } else {
-        lj = D - 1;  // past the range: reload the last slice (never read; keeps the counts uniform)
+        pa += sa;
+        pb += sb;
       }
+    } else {
+      lj = D - 1;  // past the range: reload the last slice (never read; keeps the counts uniform)
     }
   };
 #pragma unroll
   for (int i = 0; i < S - 1; ++i) issue(i);
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
-  TnsLoc<D> cur = tns_locate<D>(args, b0);
+  TnsCur cur = tns_locate<D>(args, b0);
   int stage = 0;  // stage of the slice computed next
 
   for (long b = b0; b < b1; ++b) {
-    const bool do_bias = args.p[cur.p].bias_grad != nullptr && cur.bx == 0;
+    const bool do_bias = args.p[cur.p].bias_grad != nullptr && cur.bx == 0 && wn == 0;
+#pragma unroll 1
     for (int j = 0; j < D; ++j) {
-      gl_wait_vm<2 * (S - 2)>();  // this slice's two pieces landed (S - 2 younger slices may fly)
-      // the read-back as inline asm: the compiler would guard a plain LDS load with vmcnt(0)
-      // (it cannot tell the load from the ring's in-flight DMA destinations)
-      f32x4 a, bb;
-      const unsigned src = lds_off(wring + stage * 2048 + 16 * lane);
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(a), "=&v"(bb)
-                   : "v"(src));
+      gl_wait_vm<4 * (S - 2)>();     // this wave's pieces of the slice landed
+      __builtin_amdgcn_s_barrier();  // every wave's pieces landed; the previous slice fully read
+      __builtin_amdgcn_sched_barrier(0);
       issue(stage == 0 ? S - 1 : stage - 1);  // the stage read by the previous slice
+      const char* As = ring + stage * TNW_SLICE;
+      const char* Bs = As + 16384;
       stage = stage == S - 1 ? 0 : stage + 1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int ks = 0; ks < 8; ++ks) {
+        const int kr = 4 * ks + g;
+        f32x4 a;
+        f32x2 bb;
+        // inline asm: a plain LDS load would be guarded by vmcnt(0) against the ring's DMA
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b64 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(a), "=&v"(bb)
+                     : "v"(lds_off(As + kr * 512 + (64 * wm + 4 * c) * 4)),
+                       "v"(lds_off(Bs + kr * 512 + (32 * wn + 2 * c) * 4)));
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma16(a[i], bb[jj], acc[i][jj]);
-      if (do_bias) bs4 += a;
+        for (int i = 0; i < 4; ++i) {
+          acc[i][0] = mfma16(a[i], bb[0], acc[i][0]);
+          acc[i][1] = mfma16(a[i], bb[1], acc[i][1]);
+        }
+        if (do_bias) bs4 += a;
+      }
     }
-    const bool tile_end = b + 1 == b1 || b + 1 - cur.tb0 == cur.bpt;
+    const bool tile_end = b + 1 == b1 || cur.kb + 1 == cur.bpt;
+    const long tb0 = b - cur.kb;  // the tile's first block
     if (!tile_end) {
-      if (b + 1 < b1) cur = tns_locate<D>(args, b + 1);
+      tns_step<D>(args, cur);
       continue;
     }
 
     // ---- flush the tile (or this workgroup's piece of it)
     const sca_gemm_problem& P = args.p[cur.p];
-    const int m0 = cur.by * 64, n0 = cur.bx * 64;
-    float* bred = red + 8 * 1024;
-    if (do_bias) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bs4[q] += __shfl_xor(bs4[q], 16, 64);
-        bs4[q] += __shfl_xor(bs4[q], 32, 64);
-      }
+    const int m0 = cur.by * TNW_T, n0 = cur.bx * TNW_T;
+    const bool bias_tile = P.bias_grad != nullptr && cur.bx == 0;
+    // bias: wave (wm, 0) lane (g, c) holds 4 rows' partial sums over its k group g
+    if (do_bias) st4(&bred[wm][g][4 * c], bs4);
+    lds_barrier();
+    float bsum = 0.f;  // thread t < 128: row m0 + t
+    if (bias_tile && threadIdx.x < TNW_T) {
+      const int r = threadIdx.x & 63, h = threadIdx.x >> 6;
+      bsum = (bred[h][0][r] + bred[h][1][r]) + (bred[h][2][r] + bred[h][3][r]);
     }
-    f32x4 sum[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      lds_barrier();  // the previous pass's (or flush's) reads are done
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        st4(red + wave * 1024 + ((g * 4 + i) * 16 + c) * 4,
-            f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]});
-      if (r == 0 && do_bias && g == 0) st4(bred + wave * 64 + 4 * c, bs4);
-      lds_barrier();
-      if (t < 256) {
-        f32x4 s4 = ld4(red + 4 * t);
-#pragma unroll
-        for (int ww = 1; ww < 8; ++ww) s4 += ld4(red + ww * 1024 + 4 * t);
-        sum[r] = s4;
-      }
-    }
-    float bsum = 0.f;
-    if (do_bias && t < 64) {
-#pragma unroll
-      for (int ww = 0; ww < 8; ++ww) bsum += bred[ww * 64 + t];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     bs4 = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const long tb1 = cur.tb0 + cur.bpt;
-    const int wa = (int)(((cur.tb0 + 1) * G - 1) / TB), wb = (int)((tb1 * G - 1) / TB);
+    const long tb1 = tb0 + cur.bpt;
+    const int wa = (int)(((tb0 + 1) * G - 1) / TB), wb = (int)((tb1 * G - 1) / TB);
     const float alpha = P.seg[0].alpha;
+    // element e = (i, j, r) of this lane: row m0 + 64 wm + 16 g + 4 r + i, column n0 + 32 wn + 2c + j;
+    // slab offset of the float2 (j = 0, 1) of (r, i)
+    auto soff = [&](int r, int i) { return (64 * wm + 16 * g + 4 * r + i) * TNW_T + 32 * wn + 2 * c; };
     bool finish = wa == wb;  // the whole tile was this workgroup's
     if (!finish) {
-      // write this piece (slot 0 if the tile is the one this workgroup's range starts in)
-      const int slot = b0 >= cur.tb0 ? 0 : 1;
-      float* slab = args.ws + (long)(2 * w + slot) * 4096;
-      float* bslab = args.ws + (long)G * 2 * 4096 + (long)(2 * w + slot) * 64;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, 4096 * 4, 0x00020000);
-      if (t < 256) {
+      const int slot = b0 >= tb0 ? 0 : 1;
+      float* slab = args.ws + (long)(2 * w + slot) * TNW_SLAB;
+      float* bslab = args.ws + (long)G * 2 * TNW_SLAB + (long)(2 * w + slot) * TNW_T;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, TNW_SLAB * 4, 0x00020000);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const f32x4 x = sum[r];
-          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs,
-                                                 ((16 * tg + 4 * r + ti) * 64 + 4 * tc) * 4, 0, 16);
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 x = {acc[i][0][r], acc[i][1][r]};
+          __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<const __attribute__((ext_vector_type(2))) unsigned*>(&x),
+                                                rs, soff(r, i) * 4, 0, 16);
         }
-      }
-      if (do_bias && t < 64) __hip_atomic_store(bslab + t, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (bias_tile && threadIdx.x < TNW_T)
+        __hip_atomic_store(bslab + threadIdx.x, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
       __syncthreads();
       unsigned* cnt = args.counters + cur.tile;
-      if (t == 0)
+      if (threadIdx.x == 0)
         flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(wb - wa);
       __syncthreads();
       finish = flag != 0;
       if (finish) {
-        if (t == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded
-        f32x4 tot[4];
+        f32x4 tot[4][2];
         float btot = 0.f;
         for (int wq = wa; wq <= wb; ++wq) {  // pieces in k order
           const long q0 = (long)wq * TB / G;
-          const int sq = q0 >= cur.tb0 ? 0 : 1;
+          const int sq = q0 >= tb0 ? 0 : 1;
           const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-              args.ws + (long)(2 * wq + sq) * 4096, 0, 4096 * 4, 0x00020000);
-          const float* bq = args.ws + (long)G * 2 * 4096 + (long)(2 * wq + sq) * 64;
-          if (t < 256) {
+              args.ws + (long)(2 * wq + sq) * TNW_SLAB, 0, TNW_SLAB * 4, 0x00020000);
+          const float* bq = args.ws + (long)G * 2 * TNW_SLAB + (long)(2 * wq + sq) * TNW_T;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const f32x4 x = wq == w ? sum[r] : ld4_sc1(rq, (16 * tg + 4 * r + ti) * 64 + 4 * tc);
-              tot[r] = wq == wa ? x : tot[r] + x;
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              f32x2 x;
+              if (wq == w) {
+                x = f32x2{acc[i][0][r], acc[i][1][r]};
+              } else {
+                const auto u = __builtin_amdgcn_raw_buffer_load_b64(rq, soff(r, i) * 4, 0, 16);
+                x = *reinterpret_cast<const f32x2*>(&u);
+              }
+              if (wq == wa) {
+                tot[i][0][r] = x[0];
+                tot[i][1][r] = x[1];
+              } else {
+                tot[i][0][r] += x[0];
+                tot[i][1][r] += x[1];
+              }
             }
-          }
-          if (do_bias && t < 64) {
-            const float x = wq == w ? bsum : __hip_atomic_load(bq + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (bias_tile && threadIdx.x < TNW_T) {
+            const float x = wq == w ? bsum : __hip_atomic_load(bq + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             btot = wq == wa ? x : btot + x;
           }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sum[r] = tot[r];
+        for (int i = 0; i < 4; ++i) {
+          acc[i][0] = tot[i][0];
+          acc[i][1] = tot[i][1];
+        }
         bsum = btot;
       }
     }
     if (finish) {
-      if (do_bias && t < 64 && m0 + t < P.M) P.bias_grad[m0 + t] = bsum * alpha * P.bias_grad_scale;
-      if (t < 256) {
-        const int n = n0 + 4 * tc;
-        DropMask dm;
-        if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+      if (bias_tile && threadIdx.x < TNW_T && m0 + (int)threadIdx.x < P.M)
+        P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
+      const int n = n0 + 32 * wn + 2 * c;
+      DropMask dm;
+      if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+      if (n < P.N) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + 16 * tg + 4 * r + ti;
-          if (m >= P.M || n >= P.N) continue;
-          f32x4 o = (sum[r] * alpha + (P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f})) * P.post_scale;
-          if (P.epi & SCA_EPI_GELU) {
-            st4(P.aux_out + (long)m * P.ldo + n, o);
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
+          for (int i = 0; i < 4; ++i) {
+            const int m = m0 + 64 * wm + 16 * g + 4 * r + i;
+            if (m >= P.M) continue;
+            f32x2 o = f32x2{acc[i][0][r], acc[i][1][r]} * alpha;
+            if (P.bias) o += f32x2{P.bias[n], P.bias[n + 1]};
+            o *= P.post_scale;
+            if (P.epi & SCA_EPI_GELU) {
+              *(f32x2*)(P.aux_out + (long)m * P.ldo + n) = o;
+              o[0] = gelu_erf(o[0]);
+              o[1] = gelu_erf(o[1]);
+            }
+            if (P.epi & SCA_EPI_DROPOUT) {
+              o[0] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)n, o[0]);
+              o[1] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + 1), o[1]);
+            }
+            if (P.epi & SCA_EPI_DGELU) {
+              const f32x2 ax = *(const f32x2*)(P.aux + (long)m * P.ldx + n);
+              o[0] *= gelu_erf_grad(ax[0]);
+              o[1] *= gelu_erf_grad(ax[1]);
+            }
+            f32x2 ex = {0.f, 0.f};
+            if (P.resid) ex += *(const f32x2*)(P.resid + (long)m * P.ldr + n);
+            if (P.epi & SCA_EPI_ACCUM) ex += *(const f32x2*)(P.C + (long)m * P.ldc + n);
+            *(f32x2*)(P.C + (long)m * P.ldc + n) = o + ex;
           }
-          if (P.epi & SCA_EPI_DROPOUT) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), o[j]);
-          }
-          if (P.epi & SCA_EPI_DGELU) {
-            const f32x4 ax = ld4(P.aux + (long)m * P.ldx + n);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
-          }
-          f32x4 ex = {0.f, 0.f, 0.f, 0.f};
-          if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
-          if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
-          st4(P.C + (long)m * P.ldc + n, o + ex);
-        }
       }
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     gl_wait_vm<0>();  // the flush's own memory operations shifted the ring's counts
-    if (b + 1 < b1) cur = tns_locate<D>(args, b + 1);
+    lds_barrier();    // bred is rewritten by the next flush
+    tns_step<D>(args, cur);
   }
 }
 
@@ -2072,7 +2106,7 @@ int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
 
 template <int D>
 int launch_tns(const GemmArgs& a, int nwg, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_tns_kernel<D, 4>), dim3(nwg), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((gemm_tns_kernel<D, 3>), dim3(nwg), dim3(512), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -2292,12 +2326,12 @@ int cu_count() {
 
 extern "C" long sca_gemm_tn_streamk_workspace(int nwg) {
   if (nwg <= 0) nwg = cu_count();
-  return (long)nwg * 2 * (4096 + 64);
+  return (long)nwg * 2 * (TNW_SLAB + TNW_T);
 }
 
 extern "C" long sca_gemm_tn_streamk_tiles(int nprob, const sca_gemm_problem* probs) {
   long n = 0;
-  for (int i = 0; i < nprob; ++i) n += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
+  for (int i = 0; i < nprob; ++i) n += (long)((probs[i].M + TNW_T - 1) / TNW_T) * ((probs[i].N + TNW_T - 1) / TNW_T);
   return n;
 }
 
@@ -2326,7 +2360,7 @@ extern "C" int sca_gemm_tn_streamk(int nprob, const sca_gemm_problem* probs, int
   long tb = 0;
   for (int i = 0; i < nprob; ++i) {
     a.p[i] = probs[i];
-    tb += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64) * (probs[i].seg[0].K / (32 * D));
+    tb += (long)((probs[i].M + TNW_T - 1) / TNW_T) * ((probs[i].N + TNW_T - 1) / TNW_T) * (probs[i].seg[0].K / (32 * D));
   }
   if (tb == 0) return SCA_OK;
   if (nwg > tb) nwg = (int)tb;

@@ -1,0 +1,11 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r05tn2
+mkdir -p $O
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?
+         echo "[$name] rc=$rc"; tail -n ${TAILN:-4} "$O/$name.log" | cut -c1-300; return $rc; }
+step tn_tests 300 python -u -m pytest tests/test_gpu_gemm_tn.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit 1
+TAILN=12 step full 200 python -u tools/tn_streamk_bench.py --only cfg2 || exit 1
+TAILN=12 step s6 200 env SCA_TNS_STAGES=6 python -u tools/tn_streamk_bench.py --only cfg2 --streamk-only || exit 1
+TAILN=12 step nodma 200 env SCA_TNS_PROBE=1 python -u tools/tn_streamk_bench.py --only cfg2 --streamk-only || exit 1
+TAILN=12 step nomfma 200 env SCA_TNS_PROBE=2 python -u tools/tn_streamk_bench.py --only cfg2 --streamk-only || exit 1
