@@ -1079,12 +1079,8 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
     sb = 32L * Sg.ldb;
   };
   ptrs();
-  auto issue = [&](int stage) {
-    char* dst = ring + stage * TNW_SLICE + wave * 2048;  // image rows 4w .. 4w+3 (512 B each)
-    gl_dma(pa, dst);
-    gl_dma(pa + 2 * (sa >> 5), dst + 1024);
-    gl_dma(pb, dst + 16384);
-    gl_dma(pb + 2 * (sb >> 5), dst + 16384 + 1024);
+  // the load cursor past one slice
+  auto advance = [&]() {
     if (++lj < D) {
       pa += sa;
       pb += sb;
@@ -1102,7 +1098,14 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
     }
   };
 #pragma unroll
-  for (int i = 0; i < S - 1; ++i) issue(i);
+  for (int i = 0; i < S - 1; ++i) {  // prologue: the first S - 1 slices
+    char* dst = ring + i * TNW_SLICE + wave * 2048;  // image rows 4w .. 4w+3 (512 B each)
+    gl_dma(pa, dst);
+    gl_dma(pa + 2 * (sa >> 5), dst + 1024);
+    gl_dma(pb, dst + 16384);
+    gl_dma(pb + 2 * (sb >> 5), dst + 16384 + 1024);
+    advance();
+  }
 
   f32x4 acc[4][2];
 #pragma unroll
@@ -1118,27 +1121,44 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
       gl_wait_vm<4 * (S - 2)>();     // this wave's pieces of the slice landed
       __builtin_amdgcn_s_barrier();  // every wave's pieces landed; the previous slice fully read
       __builtin_amdgcn_sched_barrier(0);
-      issue(stage == 0 ? S - 1 : stage - 1);  // the stage read by the previous slice
+      const int refill = stage == 0 ? S - 1 : stage - 1;  // the stage read by the previous slice
       const char* As = ring + stage * TNW_SLICE;
       const char* Bs = As + 16384;
       stage = stage == S - 1 ? 0 : stage + 1;
+      // fragments double-buffered in registers: k-step ks + 1's reads are issued before
+      // k-step ks's MFMAs and waited for after them (inline asm: a plain LDS load would be
+      // guarded by vmcnt(0) against the ring's DMA; the waits tie the registers they cover)
+      const unsigned ao = lds_off(As + (64 * wm + 4 * c) * 4 + g * 512);
+      const unsigned bo = lds_off(Bs + (32 * wn + 2 * c) * 4 + g * 512);
+      f32x4 a[2];
+      f32x2 bb[2];
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b64 %1, %3" : "=&v"(a[0]), "=&v"(bb[0]) : "v"(ao), "v"(bo));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(bb[0]));
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
-        const int kr = 4 * ks + g;
-        f32x4 a;
-        f32x2 bb;
-        // inline asm: a plain LDS load would be guarded by vmcnt(0) against the ring's DMA
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b64 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(a), "=&v"(bb)
-                     : "v"(lds_off(As + kr * 512 + (64 * wm + 4 * c) * 4)),
-                       "v"(lds_off(Bs + kr * 512 + (32 * wn + 2 * c) * 4)));
+        const int cb = ks & 1, nb = cb ^ 1;
+        if (ks < 7)
+          asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b64 %1, %3 offset:%4"
+                       : "=&v"(a[nb]), "=&v"(bb[nb])
+                       : "v"(ao), "v"(bo), "i"((ks + 1) * 2048));
+        if (ks == 1 || ks == 3) {  // the refill's DMA pieces spread over the slice: A at k-step 1, B at 3
+          char* dst = ring + refill * TNW_SLICE + wave * 2048 + (ks == 3 ? 16384 : 0);
+          const float* src = ks == 3 ? pb : pa;
+          const long rs = ks == 3 ? (sb >> 5) : (sa >> 5);
+          gl_dma(src, dst);
+          gl_dma(src + 2 * rs, dst + 1024);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          acc[i][0] = mfma16(a[i], bb[0], acc[i][0]);
-          acc[i][1] = mfma16(a[i], bb[1], acc[i][1]);
+          acc[i][0] = mfma16(a[cb][i], bb[cb][0], acc[i][0]);
+          acc[i][1] = mfma16(a[cb][i], bb[cb][1], acc[i][1]);
         }
-        if (do_bias) bs4 += a;
+        if (do_bias) bs4 += a[cb];
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks < 7) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[nb]), "+v"(bb[nb]));
       }
+      advance();  // the load cursor past the slice just issued
     }
     const bool tile_end = b + 1 == b1 || cur.kb + 1 == cur.bpt;
     const long tb0 = b - cur.kb;  // the tile's first block
