@@ -1045,7 +1045,7 @@ __device__ __forceinline__ unsigned lds_off(const char* p) {
 }
 
 template <int D, int S>
-__global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
+__global__ __launch_bounds__(256) void gemm_tns_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(1024))) char ring[S * TNW_SLICE];
   __shared__ float bred[2][4][64];  // bias partials: [wm][g][64 rows]
   __shared__ unsigned flag;
@@ -1058,12 +1058,12 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave >> 1, wn = wave & 1;
 
   // load cursor: the slice loaded next and this lane's DMA sources in it (wave w loads image
-  // rows 4w .. 4w+3 of A and of B: pieces q = 0, 1 of two k rows each; lane -> row lane >> 5,
-  // columns 4 (lane & 31) .. +3); within a tile consecutive blocks are consecutive k, so the
-  // pointers just advance by a slice — recomputed only when a new tile starts
+  // rows 8w .. 8w+7 of A and of B, four 2-row pieces each; lane -> row lane >> 5, columns
+  // 4 (lane & 31) .. +3); within a tile consecutive blocks are consecutive k, so the pointers
+  // just advance by a slice — recomputed only when a new tile starts
   TnsCur lc = tns_locate<D>(args, b0);
   long lrem = b1 - b0;
   int lj = 0;
@@ -1072,7 +1072,7 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
   auto ptrs = [&]() {
     const sca_gemm_problem& P = args.p[lc.p];
     const sca_gemm_seg& Sg = P.seg[0];
-    const long k = (long)lc.kb * (32 * D) + 4 * wave + (lane >> 5);
+    const long k = (long)lc.kb * (32 * D) + 8 * wave + (lane >> 5);
     pa = Sg.A + k * Sg.lda + min(lc.by * TNW_T + 4 * (lane & 31), P.M - 4);
     pb = Sg.B + k * Sg.ldb + min(lc.bx * TNW_T + 4 * (lane & 31), P.N - 4);
     sa = 32L * Sg.lda;
@@ -1097,19 +1097,26 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
       lj = D - 1;  // past the range: reload the last slice (never read; keeps the counts uniform)
     }
   };
+  // DMA piece q (0..7) of this wave's share of the slice at the cursor into stage `st`:
+  // q < 4: A rows 8w + 2q, +1;  q >= 4: B rows 8w + 2(q-4), +1
+  auto piece = [&](int st, int q) {
+    const bool isb = q >= 4;
+    const int qq = q & 3;
+    char* dst = ring + st * TNW_SLICE + (isb ? 16384 : 0) + (8 * wave + 2 * qq) * 512;
+    gl_dma((isb ? pb : pa) + 2 * qq * ((isb ? sb : sa) >> 5), dst);
+  };
 #pragma unroll
   for (int i = 0; i < S - 1; ++i) {  // prologue: the first S - 1 slices
-    char* dst = ring + i * TNW_SLICE + wave * 2048;  // image rows 4w .. 4w+3 (512 B each)
-    gl_dma(pa, dst);
-    gl_dma(pa + 2 * (sa >> 5), dst + 1024);
-    gl_dma(pb, dst + 16384);
-    gl_dma(pb + 2 * (sb >> 5), dst + 16384 + 1024);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) piece(i, q);
     advance();
   }
 
-  f32x4 acc[4][2];
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
   TnsCur cur = tns_locate<D>(args, b0);
   int stage = 0;  // stage of the slice computed next
@@ -1118,7 +1125,7 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
     const bool do_bias = args.p[cur.p].bias_grad != nullptr && cur.bx == 0 && wn == 0;
 #pragma unroll 1
     for (int j = 0; j < D; ++j) {
-      gl_wait_vm<4 * (S - 2)>();     // this wave's pieces of the slice landed
+      gl_wait_vm<8 * (S - 2)>();     // this wave's pieces of the slice landed
       __builtin_amdgcn_s_barrier();  // every wave's pieces landed; the previous slice fully read
       __builtin_amdgcn_sched_barrier(0);
       const int refill = stage == 0 ? S - 1 : stage - 1;  // the stage read by the previous slice
@@ -1129,31 +1136,23 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
       // k-step ks's MFMAs and waited for after them (inline asm: a plain LDS load would be
       // guarded by vmcnt(0) against the ring's DMA; the waits tie the registers they cover)
       const unsigned ao = lds_off(As + (64 * wm + 4 * c) * 4 + g * 512);
-      const unsigned bo = lds_off(Bs + (32 * wn + 2 * c) * 4 + g * 512);
-      f32x4 a[2];
-      f32x2 bb[2];
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b64 %1, %3" : "=&v"(a[0]), "=&v"(bb[0]) : "v"(ao), "v"(bo));
+      const unsigned bo = lds_off(Bs + (64 * wn + 4 * c) * 4 + g * 512);
+      f32x4 a[2], bb[2];
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(a[0]), "=&v"(bb[0]) : "v"(ao), "v"(bo));
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(bb[0]));
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int cb = ks & 1, nb = cb ^ 1;
         if (ks < 7)
-          asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b64 %1, %3 offset:%4"
+          asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b128 %1, %3 offset:%4"
                        : "=&v"(a[nb]), "=&v"(bb[nb])
                        : "v"(ao), "v"(bo), "i"((ks + 1) * 2048));
-        if (ks == 1 || ks == 3) {  // the refill's DMA pieces spread over the slice: A at k-step 1, B at 3
-          char* dst = ring + refill * TNW_SLICE + wave * 2048 + (ks == 3 ? 16384 : 0);
-          const float* src = ks == 3 ? pb : pa;
-          const long rs = ks == 3 ? (sb >> 5) : (sa >> 5);
-          gl_dma(src, dst);
-          gl_dma(src + 2 * rs, dst + 1024);
-        }
+        piece(refill, ks);  // the refill's DMA: one piece per k-step
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[i][0] = mfma16(a[cb][i], bb[cb][0], acc[i][0]);
-          acc[i][1] = mfma16(a[cb][i], bb[cb][1], acc[i][1]);
-        }
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma16(a[cb][i], bb[cb][jj], acc[i][jj]);
         if (do_bias) bs4 += a[cb];
         __builtin_amdgcn_sched_barrier(0);
         if (ks < 7) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[nb]), "+v"(bb[nb]));
@@ -1184,10 +1183,11 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
     const long tb1 = tb0 + cur.bpt;
     const int wa = (int)(((tb0 + 1) * G - 1) / TB), wb = (int)((tb1 * G - 1) / TB);
     const float alpha = P.seg[0].alpha;
-    // element e = (i, j, r) of this lane: row m0 + 64 wm + 16 g + 4 r + i, column n0 + 32 wn + 2c + j;
-    // slab offset of the float2 (j = 0, 1) of (r, i)
-    auto soff = [&](int r, int i) { return (64 * wm + 16 * g + 4 * r + i) * TNW_T + 32 * wn + 2 * c; };
+    // this lane's float4 (r, i): row 64 wm + 16 g + 4 r + i, columns 64 wn + 4c .. +3 of the tile
+    auto soff = [&](int r, int i) { return (64 * wm + 16 * g + 4 * r + i) * TNW_T + 64 * wn + 4 * c; };
+    auto row4 = [&](int r, int i) { return f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]}; };
     bool finish = wa == wb;  // the whole tile was this workgroup's
+    f32x4 tot[4][4];
     if (!finish) {
       const int slot = b0 >= tb0 ? 0 : 1;
       float* slab = args.ws + (long)(2 * w + slot) * TNW_SLAB;
@@ -1197,9 +1197,8 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const f32x2 x = {acc[i][0][r], acc[i][1][r]};
-          __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<const __attribute__((ext_vector_type(2))) unsigned*>(&x),
-                                                rs, soff(r, i) * 4, 0, 16);
+          const f32x4 x = row4(r, i);
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs, soff(r, i) * 4, 0, 16);
         }
       if (bias_tile && threadIdx.x < TNW_T)
         __hip_atomic_store(bslab + threadIdx.x, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1213,7 +1212,6 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
       if (finish) {
         if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded
-        f32x4 tot[4][2];
         float btot = 0.f;
         for (int wq = wa; wq <= wb; ++wq) {  // pieces in k order
           const long q0 = (long)wq * TB / G;
@@ -1225,73 +1223,62 @@ __global__ __launch_bounds__(512) void gemm_tns_kernel(const GemmArgs args) {
           for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              f32x2 x;
-              if (wq == w) {
-                x = f32x2{acc[i][0][r], acc[i][1][r]};
-              } else {
-                const auto u = __builtin_amdgcn_raw_buffer_load_b64(rq, soff(r, i) * 4, 0, 16);
-                x = *reinterpret_cast<const f32x2*>(&u);
-              }
-              if (wq == wa) {
-                tot[i][0][r] = x[0];
-                tot[i][1][r] = x[1];
-              } else {
-                tot[i][0][r] += x[0];
-                tot[i][1][r] += x[1];
-              }
+              const f32x4 x = wq == w ? row4(r, i) : ld4_sc1(rq, soff(r, i));
+              tot[r][i] = wq == wa ? x : tot[r][i] + x;
             }
           if (bias_tile && threadIdx.x < TNW_T) {
             const float x = wq == w ? bsum : __hip_atomic_load(bq + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             btot = wq == wa ? x : btot + x;
           }
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[i][0] = tot[i][0];
-          acc[i][1] = tot[i][1];
-        }
         bsum = btot;
       }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tot[r][i] = row4(r, i);
     }
     if (finish) {
       if (bias_tile && threadIdx.x < TNW_T && m0 + (int)threadIdx.x < P.M)
         P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
-      const int n = n0 + 32 * wn + 2 * c;
+      const int n = n0 + 64 * wn + 4 * c;
       DropMask dm;
       if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
       if (n < P.N) {
+        const f32x4 bias = P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int m = m0 + 64 * wm + 16 * g + 4 * r + i;
             if (m >= P.M) continue;
-            f32x2 o = f32x2{acc[i][0][r], acc[i][1][r]} * alpha;
-            if (P.bias) o += f32x2{P.bias[n], P.bias[n + 1]};
-            o *= P.post_scale;
+            f32x4 o = (tot[r][i] * alpha + bias) * P.post_scale;
             if (P.epi & SCA_EPI_GELU) {
-              *(f32x2*)(P.aux_out + (long)m * P.ldo + n) = o;
-              o[0] = gelu_erf(o[0]);
-              o[1] = gelu_erf(o[1]);
+              st4(P.aux_out + (long)m * P.ldo + n, o);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = gelu_erf(o[e]);
             }
             if (P.epi & SCA_EPI_DROPOUT) {
-              o[0] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)n, o[0]);
-              o[1] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + 1), o[1]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + e), o[e]);
             }
             if (P.epi & SCA_EPI_DGELU) {
-              const f32x2 ax = *(const f32x2*)(P.aux + (long)m * P.ldx + n);
-              o[0] *= gelu_erf_grad(ax[0]);
-              o[1] *= gelu_erf_grad(ax[1]);
+              const f32x4 ax = ld4(P.aux + (long)m * P.ldx + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] *= gelu_erf_grad(ax[e]);
             }
-            f32x2 ex = {0.f, 0.f};
-            if (P.resid) ex += *(const f32x2*)(P.resid + (long)m * P.ldr + n);
-            if (P.epi & SCA_EPI_ACCUM) ex += *(const f32x2*)(P.C + (long)m * P.ldc + n);
-            *(f32x2*)(P.C + (long)m * P.ldc + n) = o + ex;
+            f32x4 ex = {0.f, 0.f, 0.f, 0.f};
+            if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
+            if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
+            st4(P.C + (long)m * P.ldc + n, o + ex);
           }
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     gl_wait_vm<0>();  // the flush's own memory operations shifted the ring's counts
     lds_barrier();    // bred is rewritten by the next flush
     tns_step<D>(args, cur);
@@ -2126,7 +2113,9 @@ int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
 
 template <int D>
 int launch_tns(const GemmArgs& a, int nwg, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_tns_kernel<D, 3>), dim3(nwg), dim3(512), 0, st, a);
+  static const int stages = getenv("SCA_TNS_STAGES") ? atoi(getenv("SCA_TNS_STAGES")) : 2;  // TEMPORARY A/B
+  if (stages == 3) hipLaunchKernelGGL((gemm_tns_kernel<D, 3>), dim3(nwg), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((gemm_tns_kernel<D, 2>), dim3(nwg), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -2345,7 +2334,7 @@ int cu_count() {
 }  // namespace
 
 extern "C" long sca_gemm_tn_streamk_workspace(int nwg) {
-  if (nwg <= 0) nwg = cu_count();
+  if (nwg <= 0) nwg = 2 * cu_count();
   return (long)nwg * 2 * (TNW_SLAB + TNW_T);
 }
 
@@ -2370,7 +2359,7 @@ extern "C" int sca_gemm_tn_streamk(int nprob, const sca_gemm_problem* probs, int
                   "slices per block, M, N >= 4 and M, N, lda, ldb, ldc multiples of 4, 16-byte aligned operands");
     return SCA_ERR_ARG;
   }
-  if (nwg <= 0) nwg = cu_count();
+  if (nwg <= 0) nwg = 2 * cu_count();  // two 4-wave workgroups per CU (64 KB of LDS each)
   GemmArgs a;
   a.splitk = 1;
   a.ws = workspace;

@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r05tn4
+mkdir -p $O
+step() { local name=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?
+         echo "[$name] rc=$rc"; tail -n ${TAILN:-4} "$O/$name.log" | cut -c1-300; return $rc; }
+step tn_tests 300 python -u -m pytest tests/test_gpu_gemm_tn.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit 1
+step s2 300 python -u tools/tn_streamk_bench.py || exit 1
+step s3 300 env SCA_TNS_STAGES=3 python -u tools/tn_streamk_bench.py --streamk-only || exit 1

@@ -32,7 +32,7 @@ def probs(c):
 def variants(c):
     P = probs(c)
     out = []
-    for nwg in (256, 128):
+    for nwg in (512, 256):
         for spb in (4, 8):
             out.append((f"streamK nwg={nwg} spb={spb}", lambda nwg=nwg, spb=spb: ops.gemm_tn_streamk(P, nwg, spb)))
     tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="", help="comma-separated substrings of case names to run")
     ap.add_argument("--streamk-only", action="store_true")
+    ap.add_argument("--profile", default="", help="run the variants whose names contain this, eagerly, "
+                                                   "--iters times each, for rocprofv3 counter passes")
     args = ap.parse_args()
     torch.manual_seed(0)
     cases = [case("cfg2 attn 16x(256,256)", [(256, 256)] * 16, 2048),
@@ -62,6 +64,17 @@ def main():
              case("cfg5 attn 16x(512,512)", [(512, 512)] * 16, 8192),
              case("cfg5 fc1 4x(1536,512)", [(1536, 512)] * 4, 8192)]
     runs = []
+    if args.only:
+        cases = [c for c in cases if any(o in c["name"] for o in args.only.split(","))]
+    if args.profile:
+        for c in cases:
+            for name, fn in variants(c):
+                if any(p in name for p in args.profile.split(",")):
+                    for _ in range(args.iters):
+                        fn()
+                    torch.cuda.synchronize()
+                    print("profiled", c["name"], name, flush=True)
+        return
     print("checking + capturing", flush=True)
     for c in cases:
         print(" ", c["name"], flush=True)
