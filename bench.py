@@ -330,6 +330,13 @@ def committed_profile(args, kname, flops_per_launch):
             out["rocprof_avg_launch_us"] = round(avg_s * 1e6, 2)
             out["rocprof_source"] = f"profiles/latest/{wl}_kstats.csv (rocprofv3 --kernel-trace --stats)"
             out["_rocprof"] = (round(tf, 3), round(tf / FP32_MFMA_PEAK_TFLOPS, 4))
+    upath = os.path.join(d, f"{wl}_util.json")
+    if os.path.exists(upath):  # the kernel's MFMA busy share (SQ counters, the kernel alone)
+        for r in json.load(open(upath)):
+            if r["kernel"] == kname and r.get("mfma_busy") is not None:
+                out["mfma_busy"] = round(r["mfma_busy"], 4)
+                out["mfma_busy_source"] = (f"profiles/latest/{wl}_util.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / "
+                                           "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), counter pass: the kernel alone)")
     tpath = os.path.join(d, f"{wl}_traffic.json")
     if os.path.exists(tpath):
         tr = json.load(open(tpath)).get(kname)

@@ -1,0 +1,34 @@
+"""The profiler's kernel attribution for GEMM launches (ops._gemm_kernel_name) follows the
+launcher's eligibility rules in gemm.hip (launch_tile: vec_ok, glds_ok, tn_ok) — bench.py books
+time and FLOPs to these names.  CPU only (problem structs with stand-in addresses)."""
+from scattennet_amd import _lib as L, ops
+
+
+def _prob(M, N, K, lda, ldb, A=0x1000, B=0x2000, nseg=1, alpha2=1.0):
+    segs = [L.GemmSeg(A, B, lda, ldb, K, 1.0)] + [L.GemmSeg(A, B, lda, ldb, K, alpha2)] * (nseg - 1)
+    segs += [L.GemmSeg(None, None, 0, 0, 0, 0.0)] * (3 - nseg)
+    p = L.GemmProblem()
+    p.seg = (L.GemmSeg * 3)(*segs)
+    p.nseg, p.M, p.N, p.C, p.ldc = nseg, M, N, 0x3000, N
+    return p
+
+
+def test_tn_ksplit_tile_when_eligible():
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(256, 256, 2048, 256, 256)], 36) == "gemm_tnk_kernel<3, 1>"
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(256, 256, 2048, 256, 256)], 37) == "gemm_tnk_kernel<4, 1>"
+
+
+def test_tn_ksplit_falls_back_like_the_launcher():
+    # K not a multiple of 32: no LDS-DMA kernel -> the single-buffered register-staged TN kernel
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(64, 64, 200, 64, 64)], 36) == "gemm_kernel<2, T5>"
+    # two segments: not the k-split kernel, the 2-stage LDS-DMA one
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(64, 64, 256, 64, 64, nseg=2)], 36) == "gemm_glds_kernel<2, 2>"
+    # misaligned operand: the element-wise register-staged kernel
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(64, 64, 256, 64, 64, A=0x1004)], 36) == "gemm_kernel<2, T1, false>"
+
+
+def test_heuristic_names():
+    assert ops._gemm_kernel_name(L.GEMM_NT, [_prob(2048, 256, 256, 256, 256)], 0) == "gemm_glds_kernel<0, 3>"
+    assert ops._gemm_kernel_name(L.GEMM_NN, [_prob(2048, 256, 768, 768, 256)], 0) == "gemm_glds_kernel<1, 2>"
+    assert ops._gemm_kernel_name(L.GEMM_NN, [_prob(2046, 256, 768, 768, 256)], 0) == "gemm_kernel<1, T7>"
+    assert ops._gemm_kernel_name(L.GEMM_NT, [_prob(64, 30, 30, 30, 30)], 0) == "gemm_kernel<0, T1, false>"

@@ -1,8 +1,11 @@
-"""Weight-gradient GEMM shapes of configs 2 / 5: the stream-K kernel (sca_gemm_tn_streamk) against
-the k-split kernel (tile 36, the round-4 default) and the library (torch.bmm -> hipBLASLt), each
-checked against float64 first, timed as graph replays of 20 launches, best of 3 rounds.
+"""Weight-gradient (TN) GEMM shapes of configs 2, 3 and 5: this library's k-split kernel (tile 36,
+the launcher's choice for these launches) at split-K 2 / 3 against the library GEMM (torch.bmm ->
+hipBLASLt, no bias gradient).  Our launches are checked against float64 first and timed as graph
+replays of --iters launches; the library is timed eagerly (back-to-back launches: torch.bmm
+captured into a graph faulted with an illegal address on this ROCm, profiles/r05_tn/); best of
+--rounds.  (Round 5's stream-K kernels were measured with this tool: profiles/r05_tn/.)
 
-    python tools/tn_streamk_bench.py [--iters 20] [--rounds 3]
+    python tools/tn_library_compare.py [--iters 20] [--rounds 3] [--only cfg2,cfg3]
 """
 import argparse
 import os
@@ -32,9 +35,6 @@ def probs(c):
 def variants(c):
     P = probs(c)
     out = []
-    for nwg in (512, 256):
-        for spb in (4, 8):
-            out.append((f"streamK nwg={nwg} spb={spb}", lambda nwg=nwg, spb=spb: ops.gemm_tn_streamk(P, nwg, spb)))
     tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
     for sk in (2, 3):
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
@@ -53,14 +53,21 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="", help="comma-separated substrings of case names to run")
-    ap.add_argument("--streamk-only", action="store_true")
     ap.add_argument("--profile", default="", help="run the variants whose names contain this, eagerly, "
-                                                   "--iters times each, for rocprofv3 counter passes")
+                                                   "--iters times each, for rocprofv3 counter passes "
+                                                   "(tools/tn_pmc2.py)")
     args = ap.parse_args()
     torch.manual_seed(0)
     cases = [case("cfg2 attn 16x(256,256)", [(256, 256)] * 16, 2048),
              case("cfg2 fc1 4x(768,256)", [(768, 256)] * 4, 2048),
              case("cfg2 fc2 4x(256,768)", [(256, 768)] * 4, 2048),
+             case("cfg3 attn 12x(256,256)", [(256, 256)] * 12, 2048),
+             case("cfg3 res0 6x(256,256)", [(256, 256)] * 6, 2048),
+             case("cfg3 res1 6x(256,256)", [(256, 256)] * 6, 1024),
+             case("cfg3 res2 3x(512,512)", [(512, 512)] * 3, 1024),
+             case("cfg3 res3 6x(512,512)", [(512, 512)] * 6, 512),
+             case("cfg3 fusion se 3x(1024,512)", [(1024, 512)] * 3, 512),
+             case("cfg3 fusion inv 1x(3072,1024)", [(3072, 1024)], 512),
              case("cfg5 attn 16x(512,512)", [(512, 512)] * 16, 8192),
              case("cfg5 fc1 4x(1536,512)", [(1536, 512)] * 4, 8192)]
     runs = []
@@ -80,14 +87,12 @@ def main():
         print(" ", c["name"], flush=True)
         ref = [(dY.double().t() @ X.double(), dY.double().sum(0)) for dY, X, _, _ in c["items"]]
         for name, fn in variants(c):
-            if args.streamk_only and "streamK" not in name:
-                continue
             for _, _, dW, db in c["items"]:
                 dW.fill_(float("nan"))
                 db.fill_(float("nan"))
             fn()
             torch.cuda.synchronize()
-            if "bmm" not in name and not ("streamK" in name and os.environ.get("SCA_TNS_PROBE")):
+            if "bmm" not in name:
                 for (_, _, dW, db), (rw, rb) in zip(c["items"], ref):
                     ew = float((dW.double() - rw).abs().max() / rw.abs().max())
                     eb = float((db.double() - rb).abs().max() / rb.abs().max())
