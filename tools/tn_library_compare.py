@@ -35,6 +35,10 @@ def probs(c):
 def variants(c):
     P = probs(c)
     out = []
+    if all(ops.tn_streamk_ok(dY, X, dW) for dY, X, dW, _ in c["items"]):
+        for nwg in (512, 256):
+            for spb in (4, 8):
+                out.append((f"streamK nwg={nwg} spb={spb}", lambda nwg=nwg, spb=spb: ops.gemm_tn_streamk(P, nwg, spb)))
     tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
     for sk in (2, 3):
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
