@@ -1,9 +1,8 @@
 """Weight-gradient (TN) GEMM shapes of configs 2, 3 and 5: this library's k-split kernel (tile 36,
-the launcher's choice for these launches) at split-K 2 / 3 against the library GEMM (torch.bmm ->
-hipBLASLt, no bias gradient).  Our launches are checked against float64 first and timed as graph
-replays of --iters launches; the library is timed eagerly (back-to-back launches: torch.bmm
-captured into a graph faulted with an illegal address on this ROCm, profiles/r05_tn/); best of
---rounds.  (Round 5's stream-K kernels were measured with this tool: profiles/r05_tn/.)
+the launcher's choice for these launches) at split-K 2 / 3 and the stream-K kernel against the
+library GEMM (torch.bmm -> hipBLASLt, no bias gradient).  Our launches are checked against
+float64 first and timed as graph replays of --iters launches; the library (--library, its own
+process) eagerly, back-to-back; best of --rounds.  (Round 5's stream-K kernels were measured with this tool: profiles/r05_tn/.)
 
     python tools/tn_library_compare.py [--iters 20] [--rounds 3] [--only cfg2,cfg3]
 """
@@ -17,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
 PEAK = 157.3
+LIBRARY = False  # --library: the hipBLASLt timings only, eagerly, in a process that captures no graph
 
 
 def case(name, shapes, K):
@@ -44,7 +44,8 @@ def variants(c):
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
         out.append((f"ksplit36 sk={sk} wg={tiles * sk}", lambda sk=sk, ws=ws: ops.gemm(L.GEMM_TN, P, splitk=sk, ws=ws,
                                                                                        tile=36)))
-    if len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
+    if LIBRARY and len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
+        out.clear()
         A = torch.stack([dY for dY, _, _, _ in c["items"]])
         B = torch.stack([X for _, X, _, _ in c["items"]])
         C = torch.empty(len(c["items"]), A.shape[2], B.shape[2], device="cuda")
@@ -56,11 +57,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--library", action="store_true",
+                    help="time only torch.bmm (hipBLASLt), eagerly; without it, only this library's kernels "
+                         "(graphs): the two never share a process — round 5 saw two illegal-address faults in "
+                         "processes that mixed hipBLASLt calls with graph replays (profiles/r05_tn/)")
     ap.add_argument("--only", default="", help="comma-separated substrings of case names to run")
     ap.add_argument("--profile", default="", help="run the variants whose names contain this, eagerly, "
                                                    "--iters times each, for rocprofv3 counter passes "
                                                    "(tools/tn_pmc2.py)")
     args = ap.parse_args()
+    global LIBRARY
+    LIBRARY = args.library
     torch.manual_seed(0)
     cases = [case("cfg2 attn 16x(256,256)", [(256, 256)] * 16, 2048),
              case("cfg2 fc1 4x(768,256)", [(768, 256)] * 4, 2048),
