@@ -127,21 +127,6 @@ long sca_gemm_splitk_counters(int nprob, int maxM, int maxN);
 int sca_gemm_splitk_fused(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                           unsigned* counters, void* stream);
 
-/* Stream-K weight-gradient GEMM (TN, one segment per problem): dW = alpha * A^T B with the
- * bias gradient colsum(A) (bias_grad) and sca_gemm's epilogue, every output tile's K walked in
- * blocks of `slices_per_block` 32-k slices (4 or 8; 0: 8 where every K allows, else 4) and the
- * blocks of all tiles dealt evenly to `nwg` 4-wave workgroups (0: two per CU); a tile split
- * between workgroups is combined in-launch, in k order (deterministic).  Replaces the
- * nn.Linear weight / bias gradients of attention.py:41-44,49-51,74 and layers.py:94-108.
- * workspace: sca_gemm_tn_streamk_workspace(nwg) floats; counters:
- * sca_gemm_tn_streamk_tiles(nprob, probs) unsigned ints, ZERO on entry and left zero.
- * Requires K a positive multiple of 32 * slices_per_block, M, N >= 4 and M, N, lda, ldb,
- * ldc multiples of 4, 16-byte aligned operands; else SCA_ERR_ARG.                          */
-long sca_gemm_tn_streamk_workspace(int nwg);
-long sca_gemm_tn_streamk_tiles(int nprob, const sca_gemm_problem* probs);
-int sca_gemm_tn_streamk(int nprob, const sca_gemm_problem* probs, int nwg, int slices_per_block, float* workspace,
-                        unsigned* counters, void* stream);
-
 /* NT GEMM + post-LN LayerNorm in one launch (d_model = 256): per problem
  *   C = resid + dropout((A B^T + bias) * post_scale)      (exactly sca_gemm's NT epilogue)
  *   y = (C - mean) * rstd * gamma + beta,  rstd = 1 / sqrt(var + eps)   (nn.LayerNorm)

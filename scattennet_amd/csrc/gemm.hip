@@ -949,336 +949,6 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 }
 
-// ------------------------------------------------------------------------------ TN, stream-K
-// Weight-gradient GEMM (dW[M x N] = alpha * A^T B over K rows, A = dY [K][M], B = X [K][N],
-// both k-major; bias gradient db = colsum(dY) fused) as a stream-K launch of 8-wave
-// workgroups over 128x128 output tiles:
-//  * iteration space: every 128x128 tile of every problem, times its K in blocks of D 32-k
-//    slices; workgroup w (of G, one per CU) walks blocks [w*TB/G, (w+1)*TB/G) — whole tiles
-//    where it covers them, a head / tail piece of a tile where its range starts / ends
-//    inside one.  Every CU gets the same number of slices whatever the tile count.
-//  * 128x128 tiles halve the operand bytes per FLOP of a 64x64 tile (8 B per clock per CU at
-//    the fp32 MFMA rate).  Operands are staged the classic way, global_load_dwordx4 into
-//    registers one slice ahead and ds_write_b128 into a 2-stage LDS ring (k-major images
-//    [32 k][128], 32 KB per slice, one barrier per slice) — not LDS-DMA: round 5 measured the
-//    same loop with global_load_lds at 0.64-0.72 of peak (the DMA pieces' issue cost lands on
-//    the one wave per SIMD that also issues the MFMAs; profiles/r05_tn/).
-//  * wave (wm, wn) = (wave >> 2, wave & 3) owns rows 64 wm .. +63 and columns 32 wn .. +31.
-//    Per k-step (4 k, lane group g = lane >> 4 takes k = 4s + g) a lane reads ONE float4 of A
-//    (m = 64 wm + 4c + i) and one float2 of B (n = 32 wn + 2c + j) and feeds 8
-//    v_mfma_f32_16x16x4_f32 in outer-product form (MFMA (i, j): A component i, B component j),
-//    so a lane ends with rows 64 wm + 16g + 4r + i x columns 32 wn + 2c + j.
-//  * a tile's pieces: written write-through (sc1) to the workgroup's slab slot (0: the tile its
-//    range starts in, 1: the tile it ends in), drained, then a ticket on the tile's counter —
-//    the last piece to arrive sums them in piece (= k) order, its own from registers in its
-//    place, and runs the epilogue (the G16 recipe of the in-launch split-K combine; counters
-//    left zero).  Deterministic: k order within a lane, pieces in order.
-constexpr int TNW_T = 128;                  // tile edge
-constexpr int TNW_SLICE = 2 * 32 * TNW_T * 4;  // bytes per 32-k slice (A + B images)
-constexpr int TNW_SLAB = TNW_T * TNW_T;     // floats per slab slot
-
-// The stream-K iteration space, walked incrementally: problem p, tile row by / column bx
-// (tiles of a problem in row-major order), block kb of the tile's bpt blocks of D slices;
-// `tile` = the tile's index over all problems (its counter).  Only the workgroup's first
-// block is located by search; after that a block step is a few compares.
-struct TnsCur {
-  int p, by, bx, kb, tile;
-  int tm, tn, bpt;
-};
-
-template <int D>
-__device__ __forceinline__ void tns_shape(const GemmArgs& a, TnsCur& c) {
-  const sca_gemm_problem& P = a.p[c.p];
-  c.tm = (P.M + TNW_T - 1) / TNW_T;
-  c.tn = (P.N + TNW_T - 1) / TNW_T;
-  c.bpt = P.seg[0].K / (32 * D);
-}
-
-template <int D>
-__device__ __forceinline__ TnsCur tns_locate(const GemmArgs& a, long b) {
-  TnsCur c{0, 0, 0, 0, 0, 1, 1, 1};
-  int tbase = 0;
-  for (c.p = 0; c.p < a.nprob; ++c.p) {
-    tns_shape<D>(a, c);
-    const long n = (long)c.tm * c.tn * c.bpt;
-    if (b < n || c.p == a.nprob - 1) break;
-    b -= n;
-    tbase += c.tm * c.tn;
-  }
-  const int tile = (int)(b / c.bpt);
-  c.kb = (int)(b - (long)tile * c.bpt);
-  c.by = tile / c.tn;
-  c.bx = tile - c.by * c.tn;
-  c.tile = tbase + tile;
-  return c;
-}
-
-// next block; returns true when it starts a new tile
-template <int D>
-__device__ __forceinline__ bool tns_step(const GemmArgs& a, TnsCur& c) {
-  if (++c.kb < c.bpt) return false;
-  c.kb = 0;
-  ++c.tile;
-  if (++c.bx < c.tn) return true;
-  c.bx = 0;
-  if (++c.by < c.tm) return true;
-  c.by = 0;
-  ++c.p;
-  if (c.p < a.nprob) tns_shape<D>(a, c);
-  return true;
-}
-
-template <int D>
-__device__ __forceinline__ long tns_blocks(const GemmArgs& a) {
-  long tb = 0;
-  for (int p = 0; p < a.nprob; ++p) {
-    const sca_gemm_problem& P = a.p[p];
-    tb += (long)((P.M + TNW_T - 1) / TNW_T) * ((P.N + TNW_T - 1) / TNW_T) * (P.seg[0].K / (32 * D));
-  }
-  return tb;
-}
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-template <int D>
-__global__ __launch_bounds__(256, 2) void gemm_tns_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(1024))) char ring[2 * TNW_SLICE];
-  __shared__ float bred[2][4][64];  // bias partials: [wm][g][64 rows]
-  __shared__ unsigned flag;
-  const int G = (int)gridDim.x;
-  const unsigned orig = blockIdx.x, xcd = orig & 7, q8 = (unsigned)G >> 3, r8 = (unsigned)G & 7;
-  const int w = (int)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3));
-  const long TB = tns_blocks<D>(args);
-  const long b0 = (long)w * TB / G, b1 = (long)(w + 1) * TB / G;
-  if (b0 >= b1) return;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, c = lane & 15;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int lr = threadIdx.x >> 5, lcol = 4 * (threadIdx.x & 31);  // staging: k rows lr + 8q, columns lcol..+3
-
-  // load cursor: the slice loaded next and this thread's sources in it (A and B rows lr + 8q,
-  // q = 0..3); within a tile consecutive blocks are consecutive k, so the pointers just advance
-  // by a slice — recomputed only when a new tile starts
-  TnsCur lc = tns_locate<D>(args, b0);
-  long lrem = b1 - b0;
-  int lj = 0;
-  const float *pa, *pb;
-  long lda8, ldb8, sa, sb;
-  auto ptrs = [&]() {
-    const sca_gemm_problem& P = args.p[lc.p];
-    const sca_gemm_seg& Sg = P.seg[0];
-    const long k = (long)lc.kb * (32 * D) + lr;
-    pa = Sg.A + k * Sg.lda + min(lc.by * TNW_T + lcol, P.M - 4);
-    pb = Sg.B + k * Sg.ldb + min(lc.bx * TNW_T + lcol, P.N - 4);
-    lda8 = 8L * Sg.lda;
-    ldb8 = 8L * Sg.ldb;
-    sa = 32L * Sg.lda;
-    sb = 32L * Sg.ldb;
-  };
-  ptrs();
-  // the load cursor past one slice
-  auto advance = [&]() {
-    if (++lj < D) {
-      pa += sa;
-      pb += sb;
-    } else if (lrem > 1) {  // next block
-      lj = 0;
-      --lrem;
-      if (tns_step<D>(args, lc)) {
-        ptrs();
-      } else {
-        pa += sa;
-        pb += sb;
-      }
-    } else {
-      lj = D - 1;  // past the range: reload the last slice (never used)
-    }
-  };
-  typedef __attribute__((address_space(1))) const f32x4 gf4;
-  f32x4 stg[8];  // the slice in flight: A rows lr + 8q (q = 0..3), then B rows
-  auto load = [&]() {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      stg[q] = *(gf4*)(pa + q * lda8);
-      stg[4 + q] = *(gf4*)(pb + q * ldb8);
-    }
-    advance();
-  };
-  auto store = [&](int st) {
-    char* base = ring + st * TNW_SLICE + lcol * 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      *(f32x4*)(base + (lr + 8 * q) * 512) = stg[q];
-      *(f32x4*)(base + 16384 + (lr + 8 * q) * 512) = stg[4 + q];
-    }
-  };
-  load();
-  store(0);
-  load();
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
-  TnsCur cur = tns_locate<D>(args, b0);
-  int stage = 0;  // stage of the slice computed next
-
-  for (long b = b0; b < b1; ++b) {
-    const bool do_bias = args.p[cur.p].bias_grad != nullptr && cur.bx == 0 && wn == 0;
-#pragma unroll 1
-    for (int j = 0; j < D; ++j) {
-      __syncthreads();  // slice t's stage written by every thread; stage t+1's last reads (slice t-1) done
-      store(stage ^ 1);  // slice t + 1 (loaded during slice t - 1)
-      load();            // slice t + 2, under this slice's MFMAs
-      const float* As = reinterpret_cast<const float*>(ring + stage * TNW_SLICE) + 64 * wm + 4 * c + g * 128;
-      const float* Bs = reinterpret_cast<const float*>(ring + stage * TNW_SLICE + 16384) + 64 * wn + 4 * c + g * 128;
-      stage ^= 1;
-      // fragments double-buffered: k-step ks + 1's two reads are issued before k-step ks's 16
-      // MFMAs (scheduling barriers keep the compiler from hoisting all 16 reads of the slice)
-      f32x4 a = ld4(As), bb = ld4(Bs);
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        f32x4 an, bn;
-        if (ks < 7) {
-          an = ld4(As + (ks + 1) * 512);
-          bn = ld4(Bs + (ks + 1) * 512);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma16(a[i], bb[jj], acc[i][jj]);
-        if (do_bias) bs4 += a;
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks < 7) {
-          a = an;
-          bb = bn;
-        }
-      }
-    }
-    const bool tile_end = b + 1 == b1 || cur.kb + 1 == cur.bpt;
-    const long tb0 = b - cur.kb;  // the tile's first block
-    if (!tile_end) {
-      tns_step<D>(args, cur);
-      continue;
-    }
-
-    // ---- flush the tile (or this workgroup's piece of it)
-    const sca_gemm_problem& P = args.p[cur.p];
-    const int m0 = cur.by * TNW_T, n0 = cur.bx * TNW_T;
-    const bool bias_tile = P.bias_grad != nullptr && cur.bx == 0;
-    // bias: wave (wm, 0) lane (g, c) holds 4 rows' partial sums over its k group g
-    if (do_bias) st4(&bred[wm][g][4 * c], bs4);
-    lds_barrier();
-    float bsum = 0.f;  // thread t < 128: row m0 + t
-    if (bias_tile && threadIdx.x < TNW_T) {
-      const int r = threadIdx.x & 63, h = threadIdx.x >> 6;
-      bsum = (bred[h][0][r] + bred[h][1][r]) + (bred[h][2][r] + bred[h][3][r]);
-    }
-    bs4 = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const long tb1 = tb0 + cur.bpt;
-    const int wa = (int)(((tb0 + 1) * G - 1) / TB), wb = (int)((tb1 * G - 1) / TB);
-    const float alpha = P.seg[0].alpha;
-    // this lane's float4 (r, i): row 64 wm + 16 g + 4 r + i, columns 64 wn + 4c .. +3 of the tile
-    auto soff = [&](int r, int i) { return (64 * wm + 16 * g + 4 * r + i) * TNW_T + 64 * wn + 4 * c; };
-    auto row4 = [&](int r, int i) { return f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]}; };
-    bool finish = wa == wb;  // the whole tile was this workgroup's
-    if (!finish) {
-      const int slot = b0 >= tb0 ? 0 : 1;
-      float* slab = args.ws + (long)(2 * w + slot) * TNW_SLAB;
-      float* bslab = args.ws + (long)G * 2 * TNW_SLAB + (long)(2 * w + slot) * TNW_T;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, TNW_SLAB * 4, 0x00020000);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f32x4 x = row4(r, i);
-          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs, soff(r, i) * 4, 0, 16);
-        }
-      if (bias_tile && threadIdx.x < TNW_T)
-        __hip_atomic_store(bslab + threadIdx.x, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-      __syncthreads();
-      unsigned* cnt = args.counters + cur.tile;
-      if (threadIdx.x == 0)
-        flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(wb - wa);
-      __syncthreads();
-      finish = flag != 0;
-      if (finish) {  // every piece from its slab (this one's too: sc1-stored, drained), in k order
-        if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded
-        float btot = 0.f;
-        for (int wq = wa; wq <= wb; ++wq) {
-          const long q0 = (long)wq * TB / G;
-          const int sq = q0 >= tb0 ? 0 : 1;
-          const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-              args.ws + (long)(2 * wq + sq) * TNW_SLAB, 0, TNW_SLAB * 4, 0x00020000);
-          const float* bq = args.ws + (long)G * 2 * TNW_SLAB + (long)(2 * wq + sq) * TNW_T;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const f32x4 x = ld4_sc1(rq, soff(r, i));
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc[i][e][r] = wq == wa ? x[e] : acc[i][e][r] + x[e];
-            }
-          if (bias_tile && threadIdx.x < TNW_T) {
-            const float x = __hip_atomic_load(bq + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            btot = wq == wa ? x : btot + x;
-          }
-        }
-        bsum = btot;
-      }
-    }
-    if (finish) {
-      if (bias_tile && threadIdx.x < TNW_T && m0 + (int)threadIdx.x < P.M)
-        P.bias_grad[m0 + threadIdx.x] = bsum * alpha * P.bias_grad_scale;
-      const int n = n0 + 64 * wn + 4 * c;
-      DropMask dm;
-      if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
-      if (n < P.N) {
-        const f32x4 bias = P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int m = m0 + 64 * wm + 16 * g + 4 * r + i;
-            if (m >= P.M) continue;
-            f32x4 o = (row4(r, i) * alpha + bias) * P.post_scale;
-            if (P.epi & SCA_EPI_GELU) {
-              st4(P.aux_out + (long)m * P.ldo + n, o);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = gelu_erf(o[e]);
-            }
-            if (P.epi & SCA_EPI_DROPOUT) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + e), o[e]);
-            }
-            if (P.epi & SCA_EPI_DGELU) {
-              const f32x4 ax = ld4(P.aux + (long)m * P.ldx + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] *= gelu_erf_grad(ax[e]);
-            }
-            f32x4 ex = {0.f, 0.f, 0.f, 0.f};
-            if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
-            if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
-            st4(P.C + (long)m * P.ldc + n, o + ex);
-          }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    lds_barrier();  // bred is rewritten by the next flush
-    tns_step<D>(args, cur);
-  }
-}
-
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -2105,30 +1775,6 @@ int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-template <int D>
-int launch_tns(const GemmArgs& a, int nwg, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_tns_kernel<D>), dim3(nwg), dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
-}
-
-// the stream-K TN kernel's shape requirements (float4 operand loads and row stores, whole
-// blocks of D 32-k slices)
-bool tns_ok(const sca_gemm_problem* probs, int nprob, int D) {
-  for (int i = 0; i < nprob; ++i) {
-    const sca_gemm_problem& P = probs[i];
-    const sca_gemm_seg& S = P.seg[0];
-    if (P.nseg != 1 || P.M < 4 || P.N < 4 || (P.M & 3) || (P.N & 3) || S.K <= 0 || (S.K % (32 * D)) || !S.A ||
-        !S.B || !P.C || (S.lda & 3) || (S.ldb & 3) || (P.ldc & 3) || S.lda < P.M || S.ldb < P.N || P.ldc < P.N ||
-        ((reinterpret_cast<uintptr_t>(S.A) | reinterpret_cast<uintptr_t>(S.B) | reinterpret_cast<uintptr_t>(P.C)) & 15) ||
-        (P.resid && ((P.ldr & 3) || (reinterpret_cast<uintptr_t>(P.resid) & 15))) ||
-        (P.bias && (reinterpret_cast<uintptr_t>(P.bias) & 15)) ||
-        ((P.epi & SCA_EPI_GELU) && ((P.ldo & 3) || (reinterpret_cast<uintptr_t>(P.aux_out) & 15))) ||
-        ((P.epi & SCA_EPI_DGELU) && ((P.ldx & 3) || (reinterpret_cast<uintptr_t>(P.aux) & 15))))
-      return false;
-  }
-  return true;
-}
-
 bool tn_ok(const GemmArgs& a, int nprob) {
   for (int i = 0; i < nprob; ++i)
     if (a.p[i].nseg != 1) return false;
@@ -2310,65 +1956,6 @@ extern "C" int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* p
 extern "C" int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                                void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, false, true);
-}
-
-namespace {
-int g_cu_count = 0;
-int cu_count() {
-  if (!g_cu_count) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      g_cu_count = n;
-    if (g_cu_count <= 0) g_cu_count = 256;
-  }
-  return g_cu_count;
-}
-}  // namespace
-
-extern "C" long sca_gemm_tn_streamk_workspace(int nwg) {
-  if (nwg <= 0) nwg = 2 * cu_count();
-  return (long)nwg * 2 * (TNW_SLAB + TNW_T);
-}
-
-extern "C" long sca_gemm_tn_streamk_tiles(int nprob, const sca_gemm_problem* probs) {
-  long n = 0;
-  for (int i = 0; i < nprob; ++i) n += (long)((probs[i].M + TNW_T - 1) / TNW_T) * ((probs[i].N + TNW_T - 1) / TNW_T);
-  return n;
-}
-
-extern "C" int sca_gemm_tn_streamk(int nprob, const sca_gemm_problem* probs, int nwg, int slices_per_block,
-                                   float* workspace, unsigned* counters, void* stream) {
-  if (nprob <= 0) return SCA_OK;
-  if (nprob > SCA_GEMM_MAX_PROBLEMS || !probs || !workspace || !counters ||
-      (slices_per_block != 0 && slices_per_block != 4 && slices_per_block != 8)) {
-    sca_set_error("sca_gemm_tn_streamk: bad nprob / pointers / slices_per_block");
-    return SCA_ERR_ARG;
-  }
-  int D = slices_per_block;
-  if (!D) D = tns_ok(probs, nprob, 8) ? 8 : 4;
-  if (!tns_ok(probs, nprob, D)) {
-    sca_set_error("sca_gemm_tn_streamk: needs one segment per problem, K a positive multiple of 32 x the "
-                  "slices per block, M, N >= 4 and M, N, lda, ldb, ldc multiples of 4, 16-byte aligned operands");
-    return SCA_ERR_ARG;
-  }
-  if (nwg <= 0) nwg = 2 * cu_count();  // two 4-wave workgroups per CU (64 KB of LDS each)
-  GemmArgs a;
-  a.splitk = 1;
-  a.ws = workspace;
-  a.counters = counters;
-  a.drop_off = sca_drop_offset_ptr();
-  a.nprob = nprob;
-  long tb = 0;
-  for (int i = 0; i < nprob; ++i) {
-    a.p[i] = probs[i];
-    tb += (long)((probs[i].M + TNW_T - 1) / TNW_T) * ((probs[i].N + TNW_T - 1) / TNW_T) * (probs[i].seg[0].K / (32 * D));
-  }
-  if (tb == 0) return SCA_OK;
-  if (nwg > tb) nwg = (int)tb;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int rc = D == 8 ? launch_tns<8>(a, nwg, st) : launch_tns<4>(a, nwg, st);
-  if (rc != SCA_OK) sca_set_error("sca_gemm_tn_streamk: launch failed");
-  return rc;
 }
 
 extern "C" long sca_gemm_splitk_counters(int nprob, int maxM, int maxN) {

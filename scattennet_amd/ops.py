@@ -8,7 +8,6 @@ Activations are contiguous (B, T, C) fp32 on the GPU, viewed as (M = B*T, C) row
 Parameters keep the nn.Linear / nn.LayerNorm layouts of the reference (W is [out, in]).
 """
 import ctypes
-import os
 
 import torch
 from torch.autograd import Function
@@ -249,40 +248,6 @@ def gemm(layout, probs, splitk=1, ws=None, tile=0):
         if splitk > 1:  # the fixed-order slab reduction: its own launch (timed apart)
             with _timed("splitk_reduce4_kernel", 0.0):
                 L.check(lib.sca_gemm_reduce(layout, len(chunk), arr, splitk, ptr(ws), st), "sca_gemm_reduce")
-
-
-# weight gradients on the stream-K kernel (sca_gemm_tn_streamk) wherever the shapes allow it
-_TN_STREAMK = os.environ.get("SCA_TN_STREAMK", "1") != "0"  # SCA_TN_STREAMK=0: the round-4 kernels (A/B)
-_TN_STREAMK_NWG = 0        # workgroups: 0 = one per CU
-_TN_STREAMK_SPB = 0        # 32-k slices per stream-K block: 0 = 8 where K allows, else 4
-
-
-def tn_streamk_ok(dY, X, W):
-    """The stream-K weight-gradient kernel's requirements for dW = dY^T X (dY [K, M], X [K, N])."""
-    K, M = dY.shape
-    N = X.shape[1]
-    return (_TN_STREAMK and K > 0 and K % 128 == 0 and M >= 4 and N >= 4 and M % 4 == 0 and N % 4 == 0
-            and dY.stride(0) % 4 == 0 and X.stride(0) % 4 == 0 and dY.stride(1) == 1 and X.stride(1) == 1
-            and dY.data_ptr() % 16 == 0 and X.data_ptr() % 16 == 0)
-
-
-def gemm_tn_streamk(probs, nwg=None, spb=None):
-    """Weight-gradient GEMMs (TN, one segment each) on the stream-K kernel, up to 16 problems
-    per launch; workspace and tile counters from the caching allocator / counter ring."""
-    lib = L.lib()
-    st = L.stream_handle()
-    nwg = _TN_STREAMK_NWG if nwg is None else nwg
-    spb = _TN_STREAMK_SPB if spb is None else spb
-    dev = torch.cuda.current_device()
-    for i in range(0, len(probs), L.GEMM_MAX_PROBLEMS):
-        chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
-        arr = (L.GemmProblem * len(chunk))(*chunk)
-        ws = torch.empty(lib.sca_gemm_tn_streamk_workspace(nwg), device=torch.device("cuda", dev),
-                         dtype=torch.float32)
-        cnt = _splitk_counters(lib.sca_gemm_tn_streamk_tiles(len(chunk), arr), dev)
-        flops = sum(2.0 * p.M * p.N * p.seg[0].K for p in chunk) if _PROFILER else 0.0
-        with _timed(f"gemm_tns_kernel<{spb or 8}>", flops):
-            L.check(lib.sca_gemm_tn_streamk(len(chunk), arr, nwg, spb, ptr(ws), ptr(cnt), st), "sca_gemm_tn_streamk")
 
 
 # the fused LayerNorms' dgamma / dbeta reductions ride in the weight-gradient side section
@@ -891,15 +856,6 @@ def _weight_grads(items):
         for c in range(0, len(idxs), L.GEMM_MAX_PROBLEMS):
             sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
             tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
-            if all(tn_streamk_ok(items[i][0], items[i][1], items[i][3]) for i in sub):
-                probs = []
-                for i in sub:
-                    dY, X, alpha, W, _, bscale = items[i]
-                    n_out, n_in = W.shape
-                    probs.append(_prob([_seg(dY, X, dY.stride(0), X.stride(0), dY.shape[0], alpha)], out[i][0], n_out,
-                                       n_in, n_in, bias_grad=out[i][1], bias_grad_scale=bscale / alpha))
-                launches.append((probs, -1, None, 0))
-                continue
             sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
             tile = 0
             if (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
@@ -920,10 +876,7 @@ def _weight_grads(items):
             ws = torch.empty(wsz, device=items[0][0].device, dtype=torch.float32) if sk > 1 else None
             launches.append((probs, sk, ws, tile))
     for p, k, w, tl in launches:
-        if k < 0:
-            gemm_tn_streamk(p)
-        else:
-            gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl)
+        gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl)
     return out
 
 

@@ -1,8 +1,8 @@
 """Weight-gradient (TN) GEMM shapes of configs 2, 3 and 5: this library's k-split kernel (tile 36,
-the launcher's choice for these launches) at split-K 2 / 3 and the stream-K kernel against the
-library GEMM (torch.bmm -> hipBLASLt, no bias gradient).  Our launches are checked against
+the launcher's choice for these launches) at split-K 2 / 3 against the library GEMM (torch.bmm -> hipBLASLt, no bias gradient).  Our launches are checked against
 float64 first and timed as graph replays of --iters launches; the library (--library, its own
-process) eagerly, back-to-back; best of --rounds.  (Round 5's stream-K kernels were measured with this tool: profiles/r05_tn/.)
+process) eagerly, back-to-back; best of --rounds.  Round 5's stream-K kernels were measured with
+this tool (profiles/r05_tn/) and removed.  (Round 5's stream-K kernels were measured with this tool: profiles/r05_tn/.)
 
     python tools/tn_library_compare.py [--iters 20] [--rounds 3] [--only cfg2,cfg3]
 """
@@ -35,10 +35,6 @@ def probs(c):
 def variants(c):
     P = probs(c)
     out = []
-    if all(ops.tn_streamk_ok(dY, X, dW) for dY, X, dW, _ in c["items"]):
-        for nwg in (512, 256):
-            for spb in (4, 8):
-                out.append((f"streamK nwg={nwg} spb={spb}", lambda nwg=nwg, spb=spb: ops.gemm_tn_streamk(P, nwg, spb)))
     tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
     for sk in (2, 3):
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
