@@ -32,7 +32,13 @@ import time
 # weight-gradient side streams still overlap — +1.3 % at config 2 (tools/graph_env_sweep.sh,
 # 3 alternations: 1598 vs 1577 clips/s; 1 queue -1.6 %, 3 queues +0.2 %).  Read by the HIP
 # runtime at initialisation, so set before the first GPU call; an explicit setting wins.
-os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
+# With the data-parallel path (N > 1, or SCA_DP_FORCE) one more queue: the bucket all-reduces'
+# RCCL nodes are the second children of weight-gradient nodes (dp.GradBuckets defers their
+# fork), which the executor would put on the critical chain's queue with only two
+# (SCA_DP_GRAPH_QUEUES overrides).
+_dp_env = int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("SCA_DP_FORCE", "0") != "0"
+_GQ_USER = "DEBUG_HIP_FORCE_GRAPH_QUEUES" in os.environ
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", os.environ.get("SCA_DP_GRAPH_QUEUES", "3") if _dp_env else "2")
 
 import torch
 import torch.distributed as dist
@@ -77,8 +83,11 @@ def spawn_ranks(n):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     procs = []
+    base = dict(os.environ)
+    if not _GQ_USER:
+        base.pop("DEBUG_HIP_FORCE_GRAPH_QUEUES", None)  # each rank picks its own (the DP count)
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     status = 0

@@ -78,6 +78,9 @@ class GradBuckets:
         self.bucket_of = {}       # param index -> bucket index
         self._order, self._count = [], {}
         self._comms = {}          # False: eager communication stream, True: the capture-only one
+        # a completed bucket's all-reduce is forked at the NEXT gradient report (from events
+        # recorded when it completed): see produced()
+        self.defer = os.environ.get("SCA_DP_DEFER", "1") != "0"
         self._step = None
         self.last_fallback = []   # parameter indices reduced by the fallback in the last step
         ops.set_grad_sink(self)
@@ -102,7 +105,7 @@ class GradBuckets:
         fast = self.plan is not None and all(self.params[i].grad is None for i in self.slot)
         self._step = {"fast": fast, "pending": [len(b[2]) for b in self.plan] if fast else None,
                       "streams": [dict() for _ in self.plan] if fast else None, "works": [],
-                      "seen": set(), "producers": {}, "comms": {}}
+                      "seen": set(), "producers": {}, "comms": {}, "ready": []}
         torch.autograd.Variable._execution_engine.queue_callback(self._finish)
 
     # ------------------------------------------------------------------ sink protocol (ops)
@@ -121,6 +124,7 @@ class GradBuckets:
         if self._step is None:
             self._begin()
         st = self._step
+        self._launch_ready()  # buckets completed at the previous report
         stream = self._stream()
         if stream is not None:
             st["producers"][stream.cuda_stream] = stream
@@ -141,12 +145,40 @@ class GradBuckets:
                 st["streams"][b][stream.cuda_stream] = stream
             st["pending"][b] -= 1
             if st["pending"][b] == 0 and self.overlap and self.collective:
-                self._launch(b)
+                if self.defer and self.params[0].is_cuda:
+                    st["ready"].append((b, self._ready_events(b)))
+                else:
+                    self._launch(b)
 
     # ------------------------------------------------------------------ collectives
     def _bucket(self, b):
         o, n, _ = self.plan[b]
         return self.flat[o:o + n]
+
+    def _ready_events(self, b):
+        """Events on every stream that produced bucket b's gradients, recorded now (when its
+        last gradient has just been enqueued)."""
+        evs = []
+        for s in self._step["streams"][b].values():
+            ev = torch.cuda.Event()
+            ev.record(s)
+            evs.append((ev, s))
+        return evs
+
+    def _launch_ready(self):
+        """Fork the all-reduces of the buckets completed at an earlier report.  Deferred by one
+        report so that, in the captured graph, the next weight-gradient launch is captured
+        first: it becomes the first child of the bucket's last producer and keeps that node's
+        hardware queue, and the RCCL fork is a later child (the graph executor puts a node's
+        first child on its parent's queue and later children on the next queues).
+        Forked at once, the RCCL node was the first child and moved the weight-gradient chain
+        onto the critical chain's queue: no overlap left (profiles/r05_final/dp_timeline.txt)."""
+        st = self._step
+        if not st or not st["ready"]:
+            return
+        ready, st["ready"] = st["ready"], []
+        for b, evs in ready:
+            self._launch(b, evs)
 
     def _comm_stream(self, capturing):
         st = self._comms.get(capturing)
@@ -154,21 +186,25 @@ class GradBuckets:
             st = self._comms[capturing] = torch.cuda.Stream(device=self.params[0].device)
         return st
 
-    def _on_comm(self, waits, body):
+    def _on_comm(self, waits, body, events=None):
         """Run `body` (which issues collectives in their synchronous form) on a communication
-        stream that first waits on the streams `waits`: the capture-only stream while the
-        current stream is capturing, else the eager one.  Returns the stream; the caller
-        joins it (the caller's stream must wait on it before the gradients are read)."""
+        stream that first waits on the streams `waits` (their current position) and on the
+        (event, stream) pairs `events`: the capture-only stream while the current stream is
+        capturing, else the eager one.  Returns the stream; the caller joins it (the caller's
+        stream must wait on it before the gradients are read)."""
         capturing = torch.cuda.is_current_stream_capturing()
         comm = self._comm_stream(capturing)
         for s in waits:
             comm.wait_stream(s)
             ops.note_fork(comm, s, "RCCL stream")
+        for ev, s in events or ():
+            comm.wait_event(ev)
+            ops.note_fork(comm, s, "RCCL stream")
         with torch.cuda.stream(comm):
             body()
         return comm
 
-    def _launch(self, b):
+    def _launch(self, b, events=None):
         """One AVG (or, unaveraged, SUM) all-reduce of the bucket on the communication stream forked from the bucket's producers; the CALLER's stream
         joins it at the end of the backward (under hipGraph capture a forked stream must join
         the capture's origin stream directly: a wait on it from another forked stream crashes
@@ -183,10 +219,14 @@ class GradBuckets:
         def body():  # synchronous form: enqueued on the communication stream
             dist.all_reduce(bucket, op=dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM)
 
-        comm = self._on_comm(self._step["streams"][b].values(), body)
+        if events is None:
+            comm = self._on_comm(self._step["streams"][b].values(), body)
+        else:
+            comm = self._on_comm((), body, events)
         self._step["comms"][comm.cuda_stream] = comm
 
     def _finish(self):
+        self._launch_ready()  # the last bucket(s)
         st, self._step = self._step, None
         if st is None:
             return

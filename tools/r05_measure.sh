@@ -35,3 +35,13 @@ if [ "$1" = prof ]; then
   done
   echo prof done
 fi
+if [ "$1" = dpprof ]; then
+  # the data-parallel path at world size 1 (captured bucketed RCCL all-reduces), kernel trace:
+  # one rank started directly (no launcher between rocprofv3 and the program)
+  export TMPDIR=/tmp
+  mkdir -p $out/dpprof
+  RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29633 SCA_DP_FORCE=1 \
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/dpprof -o run -- \
+    python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $out/dpprof/bench.log 2>&1 || exit $?
+  grep '"metric"' $out/dpprof/bench.log | cut -c1-300
+fi
