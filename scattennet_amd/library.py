@@ -42,7 +42,9 @@ def masked_attention(q: Tensor, k: Tensor, v: Tensor, key_valid: Optional[Tensor
 
 @masked_attention.register_fake
 def _(q, k, v, key_valid, num_heads, causal=False, causal_plus_one=False):
-    B, Tq, _ = q.shape
+    B, Tq, d = q.shape
+    if d // num_heads > 128:  # the GEMM path keeps P (B, H, Tq, Tk) instead of the row statistics
+        return torch.empty_like(q), q.new_empty(B * num_heads * Tq * k.shape[1]), q.new_empty(0)
     return torch.empty_like(q), q.new_empty(B * num_heads * Tq), q.new_empty(B * num_heads * Tq)
 
 

@@ -1005,7 +1005,8 @@ _KERNEL_HD = (16, 32, 64, 128)  # head sizes the attention kernels are built for
 def _padded_hd(hd):
     """Kernel head size for a module head size (<= 128): hd itself, or the next kernel size when the
     heads are zero-padded (exact: zero q / k columns add nothing to a score, zero v columns
-    give zero output columns and the padded gradient columns are dropped)."""
+    give zero output columns and the padded gradient columns are dropped).  Larger heads take
+    the GEMM path (_attn_fwd_gemm) before this is asked."""
     for k in _KERNEL_HD:
         if hd <= k:
             return k
@@ -1023,12 +1024,114 @@ def _unpad_heads(ts, H, hd, hdp):
             for t in ts]
 
 
-def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
-    """drop: None or (p, seeds) — attention-probability dropout, one seed per problem.
-    Head sizes other than 16 / 32 / 64 / 128 run zero-padded to the next kernel size."""
+# ---- head sizes over 128: scores through the grouped GEMM, softmax through the row kernel ----
+# The reference accepts any d_model % num_heads == 0 (attention.py:16-20); the fused attention
+# kernels are built for head sizes up to 128.  Larger heads run per (stream, clip, head) as
+#   S = q k^T + M (NT GEMM, the additive mask M as its residual operand), P = softmax_rows(S),
+#   o = P v (NN GEMM)
+# with P kept (B, H, Tq, Tk) for the backward: dP = dO v^T (NT), dv = P^T dO (TN),
+# dS = softmax_rows_bwd(P, dP), dq = dS k (NN), dk = dS^T q (TN).  M reproduces the kernels'
+# masking exactly: causal j > i -> -inf; else the materialised additive mask, or finfo.min
+# for an invalid key / +1 where causal && plus_one (include/scatten.h).
+
+def _dense_mask(B, H, Tq, Tk, causal, plus_one, key_valid, add_mask, device):
+    """(B, H or 1, Tq, Tk) additive mask with the attention kernels' semantics."""
+    if add_mask is not None:
+        m = add_mask if add_mask.dim() == 4 else add_mask[:, None]
+        m = m.clone()
+    else:
+        base = torch.full((B, 1, Tq, Tk), 1.0 if (causal and plus_one) else 0.0, device=device)
+        if key_valid is not None:
+            base = torch.where(key_valid[:, None, None, :] == 0, torch.finfo(torch.float32).min, base)
+        m = base
+    if causal:
+        above = torch.ones(Tq, Tk, dtype=torch.bool, device=device).triu(1)
+        m = m.masked_fill(above, float("-inf"))
+    return m.contiguous()
+
+
+def _raw_prob(A, B, lda, ldb, K, C, M, N, ldc, alpha=1.0, resid=None, ldr=0):
+    segs = (L.GemmSeg * 3)(L.GemmSeg(A, B, lda, ldb, K, alpha), _NOSEG, _NOSEG)
+    return L.GemmProblem(segs, 1, M, N, C, ldc, 0, None, 1.0, resid, ldr, None, 0, None, 0, None, 1.0, 0, 0.0)
+
+
+def _softmax_rows_launch(pairs, rows, N, bwd=False):
+    """pairs: [(x or y, y or dy, out)] raw pointers, each `rows` rows of N."""
+    fn = L.lib().sca_softmax_rows_bwd if bwd else L.lib().sca_softmax_rows_fwd
+    for c in range(0, len(pairs), L.SOFTMAX_MAX_PROBLEMS):
+        ch = pairs[c:c + L.SOFTMAX_MAX_PROBLEMS]
+        probs = [L.SoftmaxProblem(None, a, b, o) if bwd else L.SoftmaxProblem(a, None, None, o) for a, b, o in ch]
+        arr = (L.SoftmaxProblem * len(probs))(*probs)
+        with _timed("softmax_bwd_kernel" if bwd else "softmax_fwd_kernel", 0.0):
+            L.check(fn(len(probs), arr, rows, N, L.stream_handle()), "sca_softmax_rows_" + ("bwd" if bwd else "fwd"))
+
+
+def _attn_fwd_gemm(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop):
+    if drop:
+        raise ValueError("attention dropout with head size > 128 is not supported")
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
+    dev = q[0].device
+    mask = _dense_mask(B, H, Tq, Tk, causal, plus_one, key_valid, add_mask, dev)
+    mh = mask.shape[1]
+    o = [torch.empty_like(t) for t in q]
+    P = [torch.empty(B, H, Tq, Tk, device=dev) for _ in range(G)]
+    probs, soft = [], []
+    for g in range(G):
+        for b in range(B):
+            for h in range(H):
+                S = P[g][b, h]
+                mk = mask[b, h if mh > 1 else 0]
+                probs.append(_raw_prob(q[g].data_ptr() + 4 * (b * Tq * d + h * hd),
+                                       k[g].data_ptr() + 4 * (b * Tk * d + h * hd), d, d, hd,
+                                       S.data_ptr(), Tq, Tk, Tk, resid=mk.data_ptr(), ldr=Tk))
+                soft.append((S.data_ptr(), None, S.data_ptr()))
+    gemm(L.GEMM_NT, probs)
+    _softmax_rows_launch(soft, Tq, Tk)
+    probs = [_raw_prob(P[g][b, h].data_ptr(), v[g].data_ptr() + 4 * (b * Tk * d + h * hd), Tk, d, Tk,
+                       o[g].data_ptr() + 4 * (b * Tq * d + h * hd), Tq, hd, d)
+             for g in range(G) for b in range(B) for h in range(H)]
+    gemm(L.GEMM_NN, probs)
+    # in place of the kernels' row statistics: P (flat) and an empty tensor
+    return o, [p.view(-1) for p in P], [q[0].new_empty(0) for _ in range(G)]
+
+
+def _attn_bwd_gemm(G, H, q, k, v, P, dout, dq_scale, dv_scale):
+    B, Tq, d = q[0].shape
+    Tk = k[0].shape[1]
+    hd = d // H
+    P = [p.view(B, H, Tq, Tk) for p in P]
+    dq = [torch.empty_like(t) for t in q]
+    dk = [torch.empty_like(t) for t in k]
+    dv = [torch.empty_like(t) for t in v]
+    dS = [torch.empty_like(p) for p in P]
+    idx = [(g, b, h) for g in range(G) for b in range(B) for h in range(H)]
+    off = lambda b, h, T: 4 * (b * T * d + h * hd)  # noqa: E731
+    # dP = dO v^T  (into dS), then dS = softmax_bwd(P, dP) in place
+    gemm(L.GEMM_NT, [_raw_prob(dout[g].data_ptr() + off(b, h, Tq), v[g].data_ptr() + off(b, h, Tk), d, d, hd,
+                               dS[g][b, h].data_ptr(), Tq, Tk, Tk) for g, b, h in idx])
+    _softmax_rows_launch([(P[g][b, h].data_ptr(), dS[g][b, h].data_ptr(), dS[g][b, h].data_ptr())
+                          for g, b, h in idx], Tq, Tk, bwd=True)
+    # dv = P^T dO, dk = dS^T q (TN over the Tq rows); dq = dS k (NN)
+    gemm(L.GEMM_TN, [_raw_prob(P[g][b, h].data_ptr(), dout[g].data_ptr() + off(b, h, Tq), Tk, d, Tq,
+                               dv[g].data_ptr() + off(b, h, Tk), Tk, hd, d, alpha=dv_scale) for g, b, h in idx])
+    gemm(L.GEMM_TN, [_raw_prob(dS[g][b, h].data_ptr(), q[g].data_ptr() + off(b, h, Tq), Tk, d, Tq,
+                               dk[g].data_ptr() + off(b, h, Tk), Tk, hd, d) for g, b, h in idx])
+    gemm(L.GEMM_NN, [_raw_prob(dS[g][b, h].data_ptr(), k[g].data_ptr() + off(b, h, Tk), Tk, d, Tk,
+                               dq[g].data_ptr() + off(b, h, Tq), Tq, hd, d, alpha=dq_scale) for g, b, h in idx])
+    return dq, dk, dv
+
+
+def _attn_fwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop=None):
+    """drop: None or (p, seeds) — attention-probability dropout, one seed per problem.
+    Head sizes other than 16 / 32 / 64 / 128 run zero-padded to the next kernel size; head
+    sizes over 128 take the GEMM + row-softmax path (then `sm` is P, flat, and `sl` empty)."""
+    B, Tq, d = q[0].shape
+    Tk = k[0].shape[1]
+    hd = d // H
+    if hd > _KERNEL_HD[-1]:
+        return _attn_fwd_gemm(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop)
     hdp = _padded_hd(hd)
     if hdp != hd:
         qp, kp, vp = (_pad_heads(ts, H, hd, hdp) for ts in (q, k, v))
@@ -1056,6 +1159,8 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
+    if hd > _KERNEL_HD[-1]:  # the GEMM path: sm is P
+        return _attn_bwd_gemm(G, H, q, k, v, sm, dout, dq_scale, dv_scale)
     hdp = _padded_hd(hd)
     if hdp != hd:
         qp, kp, vp, op, dop = (_pad_heads(ts, H, hd, hdp) for ts in (q, k, v, o, dout))

@@ -45,6 +45,10 @@ CASES = [  # kind, B, Tq, Tk, d, H
     ("cross", 2, 40, 90, 384, 3),     # hd 128, Tq != Tk
     ("self", 2, 50, 50, 192, 2),      # hd 96 -> 128
     ("causal", 2, 70, 70, 160, 2),    # hd 80 -> 128
+    # head sizes over 128: scores / P V through the grouped GEMM, the row-softmax kernel
+    ("self", 2, 100, 100, 512, 2),    # hd 256
+    ("causal", 2, 70, 70, 600, 3),    # hd 200 (K not a multiple of 32: element-wise GEMM form)
+    ("cross", 2, 40, 90, 288, 1),     # hd 288, Tq != Tk
     # d_model not a multiple of 4 (element-wise GEMM loads; heads padded to 16)
     ("self", 2, 40, 40, 30, 5),       # hd 6
     ("cross", 2, 30, 50, 42, 3),      # hd 14
@@ -61,7 +65,7 @@ def test_attention_shapes_vs_oracle(kind, B, Tq, Tk, d, H, fused):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     from scattennet_amd import ops
-    if not fused and ops._padded_hd(d // H) not in (16, 32):
+    if not fused and (d // H > 128 or ops._padded_hd(d // H) not in (16, 32)):
         pytest.skip("the fused backward only exists for hd 16 and 32")
     L.lib().sca_attn_bwd_fused(fused)
     try:
@@ -70,7 +74,18 @@ def test_attention_shapes_vs_oracle(kind, B, Tq, Tk, d, H, fused):
         L.lib().sca_attn_bwd_fused(1)
 
 
-def _run_case(S, kind, B, Tq, Tk, d, H):
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["self", "causal", "cross"])
+def test_large_head_materialised_masks_vs_oracle(kind):
+    """hd 256 with the reference's own materialised masks (create_attention_mask /
+    create_causal_attention_mask semantics: the additive-mask path of the GEMM route)."""
+    import scattennet_amd as S
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    _run_case(S, kind, 2, 48, 48 if kind != "cross" else 64, 512, 2, materialised=True)
+
+
+def _run_case(S, kind, B, Tq, Tk, d, H, materialised=False):
     dev = torch.device("cuda:0")
     torch.manual_seed(Tq * 7 + Tk)
     cls = {"self": S.SelfAttention, "causal": S.SelfCausalAttention, "cross": S.CrossAttention}[kind]
@@ -86,7 +101,13 @@ def _run_case(S, kind, B, Tq, Tk, d, H):
     for b, n in enumerate(lens):
         mask[b, n:] = 0
     xg, kvg = x.to(dev).requires_grad_(True), kv.to(dev).requires_grad_(True)
-    if kind == "cross":
+    if materialised:
+        if kind == "causal":
+            am_dev = S.create_causal_attention_mask(mask.to(dev), (B, Tq), xg)
+        else:
+            am_dev = S.create_attention_mask(mask.to(dev), torch.float32, tgt_len=Tq)
+        out = m(xg, kvg, am_dev) if kind == "cross" else m(xg, am_dev)
+    elif kind == "cross":
         out = m(xg, kvg, S.key_padding_mask(mask.to(dev)))
     else:
         out = m(xg, S.key_padding_mask(mask.to(dev), causal=(kind == "causal")))
