@@ -1,4 +1,6 @@
 #include <stdlib.h>
+
+#include <type_traits>
 // Grouped fp32 GEMM on the gfx950 f32-input matrix cores (v_mfma_f32_32x32x2_f32).
 //
 // Replaces every nn.Linear forward / backward on the SCA hot path (see include/scatten.h
@@ -949,6 +951,253 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   epilogue_rows(P, rows, m0 + wm, n0 + wn, lane, args.drop_off);
 }
 
+// ------------------------------------------------------------------------------ TN, 128x128 tiles
+// Weight-gradient GEMM (dW[M x N] = A^T B, A = dY [K][M], B = X [K][N], both k-major) on
+// 128x128 tiles, 4 waves of 64x64, 64 k rows per iteration, one workgroup per CU.  The operand
+// stream is register-staged: each thread holds the NEXT iteration's 16 float4 pieces (issued
+// one iteration ahead with bounds-checked buffer loads), and the single 64-KB LDS tile is read
+// whole into registers at the top of an iteration (32 ds_read_b128 per lane: 16 k-steps x A, B),
+// so the staged pieces can be written over it while the iteration's 256 MFMAs run from
+// registers.  Per lane and k-step one float4 of A (4 consecutive m) and one of B (4 consecutive
+// n) feed 16 MFMAs in the outer-product form of gemm_tnk_kernel; a lane ends with rows
+// wm + 16g + 4r + i (g = lane >> 4; r, i < 4) x columns wn + 4c .. 4c+3 (c = lane & 15), stored
+// as float4 row pieces straight from the accumulators.  Split-K: slabs + in-launch combine
+// (gemm_glds_kernel's protocol) or the separate reduction.  Requires K % 64 == 0 per problem.
+constexpr int TB_BM = 128, TB_BK = 64;
+constexpr int TB_OP = TB_BK * TB_BM;  // floats per operand tile (32 KB)
+
+// epilogue_rows' per-piece body: one float4 of row m at columns n .. n+3
+__device__ __forceinline__ void epilogue_piece(const sca_gemm_problem& P, f32x4 v, int m, int n,
+                                               const DropMask& dm) {
+  f32x4 ex = {0.f, 0.f, 0.f, 0.f}, ax = ex;
+  if (P.resid) ex += ld4(P.resid + (long)m * P.ldr + n);
+  if (P.epi & SCA_EPI_ACCUM) ex += ld4(P.C + (long)m * P.ldc + n);
+  if (P.epi & SCA_EPI_DGELU) ax = ld4(P.aux + (long)m * P.ldx + n);
+  const f32x4 bias = P.bias ? ld4(P.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 o = (v + bias) * P.post_scale;
+  if (P.epi & SCA_EPI_GELU) {
+    st4(P.aux_out + (long)m * P.ldo + n, o);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = gelu_erf(o[j]);
+  }
+  if (P.epi & SCA_EPI_DROPOUT) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = dm.apply((uint32_t)m * (uint32_t)P.N + (uint32_t)(n + j), o[j]);
+  }
+  if (P.epi & SCA_EPI_DGELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
+  }
+  st4(P.C + (long)m * P.ldc + n, o + ex);
+}
+
+__device__ __forceinline__ f32x4 tb_load(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  return *reinterpret_cast<const f32x4*>(&r);
+}
+
+// INTER: the MFMAs of k-steps NPRE .. 15 pinned after the staged-piece stores (they cover the
+// store / load phase at one workgroup per CU, those of 0 .. NPRE-1 the fragment reads); else
+// the compiler's order (every MFMA between the fragment reads, ~216 registers: two workgroups
+// per CU cover each other's phases)
+template <bool INTER, int NPRE>
+__global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * TB_OP];
+  __shared__ unsigned flag;
+
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
+
+  const int splitk = args.splitk;
+  const int pid = bz / splitk, ks = bz % splitk;
+  const sca_gemm_problem& P = args.p[pid];
+  const int m0 = by * TB_BM, n0 = bx * TB_BM;
+  if (m0 >= P.M || n0 >= P.N) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const sca_gemm_seg& G = P.seg[0];
+  const int K = G.K;
+  const int chunk = ((K + splitk - 1) / splitk + TB_BK - 1) / TB_BK * TB_BK;
+  const int kbeg = min(K, ks * chunk), kend = min(K, kbeg + chunk);
+  const int nit = (kend - kbeg) / TB_BK;
+
+  // bounds-checked operand resources: a read past the operand's last element returns 0
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.A), 0, (int)(((long)(K - 1) * G.lda + P.M) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.B), 0, (int)(((long)(K - 1) * G.ldb + P.N) * 4), 0x00020000);
+  // thread's staged pieces j < 8: k row (tid >> 5) + 8j of the iteration, columns 4 (tid & 31) ..
+  const int srow = tid >> 5, scol = 4 * (tid & 31);
+  const int va = (int)(((long)(kbeg + srow) * G.lda + min(m0 + scol, P.M - 4)) * 4);
+  const int vb = (int)(((long)(kbeg + srow) * G.ldb + min(n0 + scol, P.N - 4)) * 4);
+  const int rowA = 8 * G.lda * 4, rowB = 8 * G.ldb * 4;       // bytes between a thread's pieces
+  const int itA = TB_BK * G.lda * 4, itB = TB_BK * G.ldb * 4;  // bytes per iteration
+  f32x4 st[16];
+  auto load = [&](int it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st[j] = tb_load(ra, va, it * itA + j * rowA);
+      st[8 + j] = tb_load(rb, vb, it * itB + j * rowB);
+    }
+  };
+  float* wbase = lds + srow * TB_BM + scol;
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st4(wbase + j * 8 * TB_BM, st[j]);
+      st4(wbase + TB_OP + j * 8 * TB_BM, st[8 + j]);
+    }
+  };
+
+  const bool do_bias = P.bias_grad != nullptr && bx == 0 && wn == 0;
+  f32x4 bs4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* ra_lds = lds + g * TB_BM + wm + 4 * c;
+  const float* rb_lds = lds + TB_OP + g * TB_BM + wn + 4 * c;
+  // one iteration: the whole LDS tile into registers, barrier, the staged pieces over it (and
+  // the loads of two iterations ahead), the 256 MFMAs, barrier
+  auto iter = [&](auto wr_c, auto ld_c, int it) {
+    constexpr bool WR = decltype(wr_c)::value, LD = decltype(ld_c)::value;
+    f32x4 a[16], b[16];
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      a[n] = ld4(ra_lds + n * 4 * TB_BM);
+      b[n] = ld4(rb_lds + n * 4 * TB_BM);
+    }
+#pragma unroll
+    for (int n = 0; n < NPRE; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[n][i], b[n][j], acc[i][j]);
+    if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WR) {
+      store();
+      if constexpr (LD) load(it + 2);
+    }
+#pragma unroll
+    for (int n = NPRE; n < 16; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[n][i], b[n][j], acc[i][j]);
+    if (do_bias) {
+#pragma unroll
+      for (int n = 0; n < 16; ++n) bs4 += a[n];
+    }
+    __syncthreads();
+  };
+  if (nit > 0) {
+    load(0);
+    store();
+    if (nit > 1) load(1);
+    __syncthreads();
+  }
+  int it = 0;
+#pragma unroll 1
+  for (; it + 2 < nit; ++it) iter(std::true_type{}, std::true_type{}, it);
+  if (it + 1 < nit) iter(std::true_type{}, std::false_type{}, it++);
+  if (it < nit) iter(std::false_type{}, std::false_type{}, it);
+
+  const float alpha = G.alpha;
+  const bool fused_k = splitk > 1 && args.counters != nullptr;
+  // bias partial: rows wm + 4c + i summed over the 4 k-lane groups (waves with wn == 0)
+  if (do_bias) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bs4[q] += __shfl_xor(bs4[q], 16, 64);
+      bs4[q] += __shfl_xor(bs4[q], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm + 4 * c + i;
+        if (m >= P.M) continue;
+        float* bp = args.ws + args.bias_off[pid] + (long)ks * P.M + m;
+        if (fused_k)
+          __hip_atomic_store(bp, bs4[i] * alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
+        else if (splitk > 1)
+          *bp = bs4[i] * alpha;
+        else
+          P.bias_grad[m] = bs4[i] * alpha * P.bias_grad_scale;
+      }
+    }
+  }
+  const int n = n0 + wn + 4 * c;
+  const bool ncol = n < P.N;
+  if (splitk > 1) {
+    const long MN = (long)P.M * P.N;
+    float* slabs = args.ws + args.slab_off[pid];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, (int)(splitk * MN * 4), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm + 16 * g + 4 * r + i;
+        if (m < P.M && ncol) {
+          const f32x4 x = f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]} * alpha;
+          const int off = (int)(((long)ks * MN + (long)m * P.N + n) * 4);
+          if (fused_k) __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs, off, 0, 16);
+          else __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&x), rs, off, 0, 0);
+        }
+      }
+    if (!fused_k) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
+    if (tid == 0)
+      flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
+    __syncthreads();
+    if (!flag) return;
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1-stored, sc1-loaded: no agent acquire
+    if (P.bias_grad && bx == 0 && tid < TB_BM && m0 + tid < P.M) {
+      float* bp = args.ws + args.bias_off[pid] + m0 + tid;
+      float t = 0.f;
+      for (int s2 = 0; s2 < splitk; ++s2)
+        t += __hip_atomic_load(bp + (long)s2 * P.M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P.bias_grad[m0 + tid] = t * P.bias_grad_scale;
+    }
+    if (!ncol) return;
+    DropMask dm;
+    if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      const int m = m0 + wm + 16 * g + q;
+      if (m >= P.M) continue;
+      const long e = (long)m * P.N + n;
+      f32x4 t = ld4_sc1(rs, e);
+      for (int s2 = 1; s2 < splitk; ++s2) t += ld4_sc1(rs, s2 * MN + e);
+      epilogue_piece(P, t, m, n, dm);
+    }
+    return;
+  }
+  if (!ncol) return;
+  DropMask dm;
+  if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm + 16 * g + 4 * r + i;
+      if (m < P.M)
+        epilogue_piece(P, f32x4{acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]} * alpha, m, n, dm);
+    }
+}
+
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -1723,15 +1972,16 @@ int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
 //   7  register-staged 128x64, 8 waves (NN fallback)
 //   20 / 21 / 22  LDS-DMA 64x64 with a 3- / 2- / 4-stage ring (the heuristic's kernels)
 //   36 / 37  TN only: the k-split outer-product weight-gradient kernel, 3- / 4-stage ring
+//   38 / 39 / 40  TN only: 128x128 tiles, register-staged operand stream (gemm_tnb_kernel<INTER, NPRE>)
 using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
 using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
 using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
-constexpr int kTnFirst = 36, kTnLast = 37;
+constexpr int kTnFirst = 36, kTnLast = 40;
 
 bool valid_tile(int layout, int tile) {
   switch (tile) {
     case 0: case 1: case 5: case 7: case 20: case 21: case 22: return true;
-    case 36: case 37: return layout == SCA_GEMM_TN;
+    case 36: case 37: case 38: case 39: case 40: return layout == SCA_GEMM_TN;
     default: return false;
   }
 }
@@ -1781,9 +2031,38 @@ bool tn_ok(const GemmArgs& a, int nprob) {
   return glds_ok(a, nprob);
 }
 
+// gemm_tnb_kernel: K a multiple of its 64-row iteration, every byte offset of the operands,
+// the slabs included, within the 32-bit range of its buffer resources
+bool tnb_ok(const GemmArgs& a, int nprob) {
+  if (!tn_ok(a, nprob)) return false;
+  const long lim = (1L << 31) - 1;
+  for (int i = 0; i < nprob; ++i) {
+    const sca_gemm_problem& P = a.p[i];
+    const sca_gemm_seg& G = P.seg[0];
+    if (G.K % TB_BK || P.M < 4 || P.N < 4) return false;
+    if (((long)G.K * G.lda + P.M) * 4 > lim || ((long)G.K * G.ldb + P.N) * 4 > lim) return false;
+    if ((long)a.splitk * P.M * P.N * 4 > lim) return false;
+  }
+  return true;
+}
+
+template <bool INTER, int NPRE>
+int launch_tnb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  dim3 grid((maxN + TB_BM - 1) / TB_BM, (maxM + TB_BM - 1) / TB_BM, nprob * a.splitk);
+  hipLaunchKernelGGL((gemm_tnb_kernel<INTER, NPRE>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
+  if (tile >= 38 && tile <= 40) {
+    if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) {
+      if (tile == 38) return launch_tnb<false, 2>(a, nprob, maxM, maxN, st);
+      return tile == 39 ? launch_tnb<true, 4>(a, nprob, maxM, maxN, st) : launch_tnb<true, 6>(a, nprob, maxM, maxN, st);
+    }
+    tile = 36;
+  }
   if (tile >= kTnFirst && tile <= kTnLast) {
     if (LAYOUT == SCA_GEMM_TN && tn_ok(a, nprob))
       return tile == 36 ? launch_tnk<3, 1>(a, nprob, maxM, maxN, st) : launch_tnk<4, 1>(a, nprob, maxM, maxN, st);

@@ -8,6 +8,7 @@ Activations are contiguous (B, T, C) fp32 on the GPU, viewed as (M = B*T, C) row
 Parameters keep the nn.Linear / nn.LayerNorm layouts of the reference (W is [out, in]).
 """
 import ctypes
+import os
 
 import torch
 from torch.autograd import Function
@@ -210,6 +211,10 @@ def _gemm_kernel_name(layout, chunk, tile):
         return f"gemm_kernel<{layout}, T1, false>"
     glds = all(p.M % 4 == 0 and p.N % 4 == 0 for p in chunk) and \
         all(g.K % 32 == 0 and g.alpha == p.seg[0].alpha for p, g in segs)
+    if t in (38, 39, 40):
+        if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
+            return {38: "gemm_tnb_kernel<false, 2>", 39: "gemm_tnb_kernel<true, 4>", 40: "gemm_tnb_kernel<true, 6>"}[t]
+        t = 36
     if t in _TILE_NAMES:
         if layout == L.GEMM_TN and glds and all(p.nseg == 1 for p in chunk):
             return _TILE_NAMES[t]
@@ -594,6 +599,29 @@ _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per
 _TNK_TILES_PER_PROBLEM = 48
 
 
+# the 128x128 register-staged weight-gradient kernel (tile 40) for long reductions (config 5:
+# K = 8192 rows); measured with tools/tn_library_compare.py: 0.82 of peak with
+# two workgroups per CU, 0.72 with one, against the k-split kernel's 0.72-0.74
+_TNB_MIN_K = int(os.environ.get("SCA_TNB_MIN_K", "4096"))  # A/B switch (0: never)
+_TNB_RATE2, _TNB_RATE1, _TNB_EPI = 0.81, 0.72, 3.0
+
+
+def _tnb_split(K, tiles128):
+    """Split-K for tile 40: the split whose estimated per-CU time is least — workgroups dealt
+    over 256 CUs, two at a time at _TNB_RATE2, a leftover one at _TNB_RATE1, plus an epilogue
+    cost per workgroup (ties: the smaller split, fewer slabs)."""
+    best, best_sk = None, 1
+    for sk in range(1, _SPLITK_MAX + 1):
+        if sk > 1 and K // sk < 1024:
+            break
+        iters = -(-(-(-K // sk)) // 64)
+        w = -(-tiles128 * sk // 256)
+        cost = (w // 2) * 2 * iters / _TNB_RATE2 + (w % 2) * iters / _TNB_RATE1 + w * _TNB_EPI
+        if best is None or cost < best - 1e-9:
+            best, best_sk = cost, sk
+    return best_sk
+
+
 def _splitk_for(M_red, n_out_tiles):
     """Split the long reduction (rows of the batch) of weight-gradient GEMMs: the split that
     fills whole rounds of the LDS-DMA kernel's 3 workgroups per CU (768 slots) best, each
@@ -858,7 +886,12 @@ def _weight_grads(items):
             tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
             sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
             tile = 0
-            if (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
+            Kr = items[sub[0]][0].shape[0]
+            if 0 < _TNB_MIN_K <= Kr and Kr % 64 == 0:
+                tile = 40
+                sk = _tnb_split(Kr, sum(-(-items[i][3].shape[0] // 128) * -(-items[i][3].shape[1] // 128)
+                                        for i in sub))
+            elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
                 # many-problem launches (an attention block's q/k/v/o of every stream) and big
                 # weights (an FFN's 768 x 256): the k-split outer-product kernel at split-K 2
                 # (tools/tn_bench.py: 16 x (256 x 256, K = 2048) 0.59-0.61 of peak vs 0.57 for

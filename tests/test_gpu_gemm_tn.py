@@ -53,11 +53,12 @@ def _check(items, alpha=1.0, bscale=1.0, base=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 37])
-@pytest.mark.parametrize("splitk,fused", [(1, False), (2, False), (2, True), (3, True)])
+@pytest.mark.parametrize("tile", [36, 37, 38, 39, 40])
+@pytest.mark.parametrize("splitk,fused", [(1, False), (2, False), (2, True), (3, True), (5, True)])
 def test_ksplit_kernel_matches_float64(tile, splitk, fused):
-    """gemm_tnk_kernel (tiles 36 / 37): M not a multiple of 64, bias on and off, split-K with the
-    in-launch (fused) and the two-launch combine."""
+    """gemm_tnk_kernel (tiles 36 / 37) and gemm_tnb_kernel (38): M not a multiple of 64 / 128,
+    bias on and off, split-K with the in-launch (fused) and the two-launch combine; split 5 of
+    K = 1024 leaves the last split empty for tile 38 (64-row chunks: 256 x 4)."""
     from scattennet_amd import _lib as L, ops
     items = _case([(100, 68), (256, 256)], 1024, seed=tile + splitk) + _case([(64, 132)], 1024, seed=3, bias=False)
     probs = _probs(items, alpha=2.0, bscale=0.25)
@@ -93,22 +94,35 @@ def _ksplit(items, tile=36, splitk=2, **kw):
 
 
 @pytest.mark.gpu
-def test_ksplit_bias_off_and_accumulate():
+def test_tnb_tile_falls_back_when_k_is_not_a_multiple_of_64():
+    """K % 64 != 0 (K % 32 == 0): tile 38 hands over to the k-split kernel."""
+    from scattennet_amd import ops
+    items = _case([(128, 128), (100, 36)], 992, seed=6)
+    probs = _probs(items)
+    assert ops._gemm_kernel_name(2, probs, 38) == "gemm_tnk_kernel<3, 1>"
+    _ksplit(items, tile=38, splitk=2)
+    _check(items)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [36, 38, 39])
+def test_ksplit_bias_off_and_accumulate(tile):
     items = _case([(128, 192)] * 3, 512, seed=5, bias=False)
     base = [torch.randn(128, 192, device="cuda") for _ in items]
     for (_, _, dW, _), b in zip(items, base):
         dW.copy_(b)
-    _ksplit(items, accum=True)
+    _ksplit(items, tile=tile, accum=True)
     _check(items, base=base)
 
 
 @pytest.mark.gpu
-def test_ksplit_is_deterministic():
+@pytest.mark.parametrize("tile", [36, 38, 39])
+def test_ksplit_is_deterministic(tile):
     """The split-K slabs are summed in slice order whichever split arrives last."""
     items = _case([(256, 256)] * 6, 2048, seed=9)
     outs = []
     for _ in range(2):
-        _ksplit(items, splitk=3)
+        _ksplit(items, tile=tile, splitk=3)
         outs.append([(dW.clone(), db.clone()) for _, _, dW, db in items])
     for (a, b), (c, d) in zip(*outs):
         assert torch.equal(a, c) and torch.equal(b, d)

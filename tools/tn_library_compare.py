@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
 PEAK = 157.3
+SPLITS = (1, 2, 3, 4, 5, 6, 8)  # --splits
 LIBRARY = False  # --library: the hipBLASLt timings only, eagerly, in a process that captures no graph
 
 
@@ -40,6 +41,14 @@ def variants(c):
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
         out.append((f"ksplit36 sk={sk} wg={tiles * sk}", lambda sk=sk, ws=ws: ops.gemm(L.GEMM_TN, P, splitk=sk, ws=ws,
                                                                                        tile=36)))
+    t128 = sum(-(-dW.shape[0] // 128) * -(-dW.shape[1] // 128) for _, _, dW, _ in c["items"])
+    for sk in SPLITS:
+        if c["K"] // sk < 256 and sk > 1:
+            continue
+        ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
+        for tl in (38, 39, 40):
+            out.append((f"tnb{tl} sk={sk} wg={t128 * sk}", lambda sk=sk, ws=ws, tl=tl: ops.gemm(
+                L.GEMM_TN, P, splitk=sk, ws=ws, tile=tl)))
     if LIBRARY and len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
         out.clear()
         A = torch.stack([dY for dY, _, _, _ in c["items"]])
@@ -61,8 +70,10 @@ def main():
     ap.add_argument("--profile", default="", help="run the variants whose names contain this, eagerly, "
                                                    "--iters times each, for rocprofv3 counter passes "
                                                    "(tools/tn_pmc2.py)")
+    ap.add_argument("--splits", default="1,2,3,4,5,6,8", help="split-K values of the 128x128 kernels")
     args = ap.parse_args()
-    global LIBRARY
+    global LIBRARY, SPLITS
+    SPLITS = tuple(int(x) for x in args.splits.split(","))
     LIBRARY = args.library
     torch.manual_seed(0)
     cases = [case("cfg2 attn 16x(256,256)", [(256, 256)] * 16, 2048),
@@ -78,6 +89,7 @@ def main():
              case("cfg5 attn 16x(512,512)", [(512, 512)] * 16, 8192),
              case("cfg5 fc1 4x(1536,512)", [(1536, 512)] * 4, 8192)]
     runs = []
+    keep = []
     if args.only:
         cases = [c for c in cases if any(o in c["name"] for o in args.only.split(","))]
     if args.profile:
@@ -113,6 +125,11 @@ def main():
             with torch.cuda.graph(g):
                 for _ in range(args.iters):
                     fn()
+            # the graph bakes in the addresses of the variant's split-K workspace, which only the
+            # lambda holds: keep it alive (every later torch.cuda.graph() capture starts with
+            # empty_cache(), which hands freed blocks back to the driver, and a replay into them
+            # faults — the cause of round 5's two "illegal address" faults in this tool)
+            keep.append(fn)
             runs.append((c, name, g))
     best = {}
     print("timing", flush=True)
