@@ -1198,6 +1198,161 @@ __global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
     }
 }
 
+// ------------------------------------------------------------------------------ NT / NN, 128x128 tiles
+// C[M x N] = sum over segments of A[M][K] B^T (NT: B [N][K]) or A B (NN: B [K][N]) (+ the
+// epilogue) on 128x128 tiles, gemm_tnb_kernel's pipeline with A k-contiguous: the staged A
+// pieces are float4 runs along k, stored to LDS as a [row][k] image with a 68-float row stride
+// (rows 16 B apart in the bank space: the 16-lane ds_read_b128 groups below are conflict-free),
+// and the fragments are the plain 16x16x4 ones — a lane's float4 at (row i, k 16kc + 4kg .. +3)
+// is its A (or B) operand of four consecutive k-steps.  NT's B is staged like A; NN's B pieces
+// (4 consecutive n at one k; a wave's 64 lanes cover 16 k x 4 pieces) are transposed into the
+// same [n][k] image by four ds_write_b32 each (64 distinct banks per instruction).  Segments
+// (dX = dQ Wq + dK Wk + dV Wv) are walked back to back.  The accumulators go through LDS
+// (per-wave 64 x 68 image) into float4 row pieces for epilogue_piece.  No split-K; every
+// segment's K % 64 == 0.
+constexpr int NB_LD = TB_BK + 4;               // 68
+constexpr int NB_OP = TB_BM * NB_LD;           // floats per operand image
+
+template <bool INTER, int NPRE, bool B_KN>
+__global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * NB_OP];
+
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned nwg = gx * gy * gridDim.z;
+  const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wgid % gx, by = (wgid / gx) % gy, pid = wgid / (gx * gy);
+  const sca_gemm_problem& P = args.p[pid];
+  const int m0 = by * TB_BM, n0 = bx * TB_BM;
+  if (m0 >= P.M || n0 >= P.N) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = lane >> 4, li = lane & 15;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nseg = P.nseg;
+  const int it0 = P.seg[0].K / TB_BK, it1 = nseg > 1 ? P.seg[1].K / TB_BK : 0;
+  const int nit = it0 + it1 + (nseg > 2 ? P.seg[2].K / TB_BK : 0);
+
+  // thread's staged pieces j < 8: A (and NT's B) row (tid >> 4) + 16j, k 4 (tid & 15) .. +3 of
+  // the iteration; NN's B: k 16 (b & 3) + (lane & 15), columns 4 (4 (b >> 2) + (lane >> 4)) ..
+  // +3 with b = 8 wave + j.  Rows / columns past the end re-read the last ones (never stored).
+  const int srow = tid >> 4, sk4 = 4 * (tid & 15);
+  f32x4 st[16];
+  auto load = [&](int it) {
+    int s = 0, lit = it;  // segment and its local iteration (wave-uniform)
+    if (lit >= it0) {
+      lit -= it0;
+      s = 1;
+      if (lit >= it1) {
+        lit -= it1;
+        s = 2;
+      }
+    }
+    const sca_gemm_seg& G = P.seg[s];
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(G.A), 0, (int)(((long)(P.M - 1) * G.lda + G.K) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(G.B), 0,
+        (int)((B_KN ? (long)(G.K - 1) * G.ldb + P.N : (long)(P.N - 1) * G.ldb + G.K) * 4), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st[j] = tb_load(ra, (int)(((long)min(m0 + srow + 16 * j, P.M - 1) * G.lda + sk4) * 4), lit * TB_BK * 4);
+      if constexpr (B_KN) {
+        const int b = 8 * wave + j;
+        const int k = 16 * (b & 3) + li, c4 = 4 * (4 * (b >> 2) + kg);
+        st[8 + j] = tb_load(rb, (int)(((long)k * G.ldb + min(n0 + c4, P.N - 4)) * 4), lit * TB_BK * G.ldb * 4);
+      } else {
+        st[8 + j] = tb_load(rb, (int)(((long)min(n0 + srow + 16 * j, P.N - 1) * G.ldb + sk4) * 4), lit * TB_BK * 4);
+      }
+    }
+  };
+  float* wbase = lds + srow * NB_LD + sk4;
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st4(wbase + j * 16 * NB_LD, st[j]);
+      if constexpr (B_KN) {
+        const int b = 8 * wave + j;
+        const int k = 16 * (b & 3) + li, c4 = 4 * (4 * (b >> 2) + kg);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lds[NB_OP + (c4 + q) * NB_LD + k] = st[8 + j][q];
+      } else {
+        st4(wbase + NB_OP + j * 16 * NB_LD, st[8 + j]);
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* ra_lds = lds + (wm + li) * NB_LD + 4 * kg;
+  const float* rb_lds = lds + NB_OP + (wn + li) * NB_LD + 4 * kg;
+  auto iter = [&](auto wr_c, auto ld_c, int it) {
+    constexpr bool WR = decltype(wr_c)::value, LD = decltype(ld_c)::value;
+    f32x4 a[4][4], b[4][4];  // [kc][block]
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[kc][q] = ld4(ra_lds + 16 * q * NB_LD + 16 * kc);
+        b[kc][q] = ld4(rb_lds + 16 * q * NB_LD + 16 * kc);
+      }
+    auto steps = [&](int t0, int t1) {
+#pragma unroll
+      for (int t = t0; t < t1; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[t >> 2][i][t & 3], b[t >> 2][j][t & 3], acc[i][j]);
+    };
+    steps(0, NPRE);
+    if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WR) {
+      store();
+      if constexpr (LD) load(it + 2);
+    }
+    steps(NPRE, 16);
+    __syncthreads();
+  };
+  load(0);
+  store();
+  if (nit > 1) load(1);
+  __syncthreads();
+  int it = 0;
+#pragma unroll 1
+  for (; it + 2 < nit; ++it) iter(std::true_type{}, std::true_type{}, it);
+  if (it + 1 < nit) iter(std::true_type{}, std::false_type{}, it++);
+  if (it < nit) iter(std::false_type{}, std::false_type{}, it);
+
+  // accumulators -> this wave's 64 x 68 image -> float4 row pieces (rows kg + 4q, columns 4 li)
+  float* img = lds + wave * 64 * NB_LD;
+  const float alpha = P.seg[0].alpha;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) img[(16 * i + 4 * kg + r) * NB_LD + 16 * j + li] = acc[i][j][r] * alpha;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int n = n0 + wn + 4 * li;
+  if (n >= P.N) return;
+  DropMask dm;
+  if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
+#pragma unroll 4
+  for (int q = 0; q < 16; ++q) {
+    const int rho = kg + 4 * q, m = m0 + wm + rho;
+    if (m < P.M) epilogue_piece(P, ld4(img + rho * NB_LD + 4 * li), m, n, dm);
+  }
+}
+
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -1973,6 +2128,7 @@ int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
 //   20 / 21 / 22  LDS-DMA 64x64 with a 3- / 2- / 4-stage ring (the heuristic's kernels)
 //   36 / 37  TN only: the k-split outer-product weight-gradient kernel, 3- / 4-stage ring
 //   38 / 39 / 40  TN only: 128x128 tiles, register-staged operand stream (gemm_tnb_kernel<INTER, NPRE>)
+//   41 / 42  NT / NN: the same with A k-contiguous (gemm_ntb_kernel<INTER, NPRE, B k-major>)
 using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
 using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
 using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
@@ -1982,6 +2138,7 @@ bool valid_tile(int layout, int tile) {
   switch (tile) {
     case 0: case 1: case 5: case 7: case 20: case 21: case 22: return true;
     case 36: case 37: case 38: case 39: case 40: return layout == SCA_GEMM_TN;
+    case 41: case 42: return layout != SCA_GEMM_TN;
     default: return false;
   }
 }
@@ -2046,6 +2203,30 @@ bool tnb_ok(const GemmArgs& a, int nprob) {
   return true;
 }
 
+// gemm_ntb_kernel: no split-K, every segment's K a positive multiple of 64 (equal alphas:
+// glds_ok), 32-bit operand offsets
+bool ntb_ok(const GemmArgs& a, int nprob, bool b_kn) {
+  if (a.splitk != 1 || !glds_ok(a, nprob)) return false;
+  const long lim = (1L << 31) - 1;
+  for (int i = 0; i < nprob; ++i) {
+    const sca_gemm_problem& P = a.p[i];
+    for (int s = 0; s < P.nseg; ++s) {
+      const sca_gemm_seg& G = P.seg[s];
+      if (G.K % TB_BK || G.K == 0) return false;
+      if (((long)P.M * G.lda + G.K) * 4 > lim) return false;
+      if ((b_kn ? (long)G.K * G.ldb + P.N : (long)P.N * G.ldb + G.K) * 4 > lim) return false;
+    }
+  }
+  return true;
+}
+
+template <bool INTER, int NPRE, bool B_KN>
+int launch_ntb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  dim3 grid((maxN + TB_BM - 1) / TB_BM, (maxM + TB_BM - 1) / TB_BM, nprob);
+  hipLaunchKernelGGL((gemm_ntb_kernel<INTER, NPRE, B_KN>), grid, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
+}
+
 template <bool INTER, int NPRE>
 int launch_tnb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + TB_BM - 1) / TB_BM, (maxM + TB_BM - 1) / TB_BM, nprob * a.splitk);
@@ -2056,6 +2237,13 @@ int launch_tnb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
+  if (tile == 41 || tile == 42) {
+    constexpr bool KN = LAYOUT == SCA_GEMM_NN;
+    if (LAYOUT != SCA_GEMM_TN && ntb_ok(a, nprob, KN))
+      return tile == 41 ? launch_ntb<true, 6, KN>(a, nprob, maxM, maxN, st)
+                        : launch_ntb<false, 2, KN>(a, nprob, maxM, maxN, st);
+    tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;
+  }
   if (tile >= 38 && tile <= 40) {
     if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) {
       if (tile == 38) return launch_tnb<false, 2>(a, nprob, maxM, maxN, st);
@@ -2080,6 +2268,17 @@ int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_
 }
 
 int g_tile_override[3] = {0, 0, 0};
+
+// SCA_NTB=0 keeps the NT / NN GEMMs on the LDS-DMA kernels (A/B switch), read once;
+// SCA_NTB_MIN_K: the shortest reduction (summed over segments) routed to the 128x128 kernel
+bool ntb_default() {
+  static const bool on = !(getenv("SCA_NTB") && atoi(getenv("SCA_NTB")) == 0);
+  return on;
+}
+int ntb_min_k() {
+  static const int k = getenv("SCA_NTB_MIN_K") ? atoi(getenv("SCA_NTB_MIN_K")) : 1024;
+  return k;
+}
 
 // Tile heuristic (measured with tools/gemm_bench.py at the workload's shapes, see
 // DESIGN.md): the 3-stage LDS-DMA 64x64 kernel wins every layout; ineligible shapes fall
@@ -2188,7 +2387,21 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   int rc;
   long tiles64 = 0;
   for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
-  const int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
+  int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
+  if (!variant && !g_tile_override[layout] && layout != SCA_GEMM_TN && splitk == 1 && tiles64 >= 2048 &&
+      ntb_default()) {
+    // big forward / input-gradient GEMMs (config 5: 8192-row operands, hundreds of 128x128
+    // tiles): the register-staged 128x128 kernel when every problem's reduction is long
+    // enough (tools/gemm_bench.py --cfg5); launch_tile hands ineligible shapes back to the
+    // LDS-DMA kernel
+    bool longk = true;
+    for (int i = 0; i < nprob; ++i) {
+      int k = 0;
+      for (int s2 = 0; s2 < probs[i].nseg; ++s2) k += probs[i].seg[s2].K;
+      longk = longk && k >= ntb_min_k();
+    }
+    if (longk) tile = 41;
+  }
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
   const bool tn_big = layout == SCA_GEMM_TN && tile >= kTnFirst && tile <= kTnLast && tn_ok(a, nprob);
   if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&

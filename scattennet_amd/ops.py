@@ -198,11 +198,16 @@ def _splitk_counters(n, device=None):
 _TILE_NAMES = {36: "gemm_tnk_kernel<3, 1>", 37: "gemm_tnk_kernel<4, 1>"}
 
 
-def _gemm_kernel_name(layout, chunk, tile):
+def _gemm_kernel_name(layout, chunk, tile, splitk=1):
     """The kernel a sca_gemm / sca_gemm_variant launch of `chunk` runs (for the profiler's
     records): the eligibility rules of gemm.hip's launch_tile (vec_ok, glds_ok, tn_ok) applied
     to the requested variant (0 = the heuristic: 3-stage LDS-DMA for NT, 2-stage otherwise)."""
     t = tile or (20 if layout == L.GEMM_NT else 21)
+    if not tile and layout != L.GEMM_TN and splitk == 1 and os.environ.get("SCA_NTB", "1") != "0" and \
+            sum(-(-p.M // 64) * -(-p.N // 64) for p in chunk) >= 2048 and \
+            all(sum(p.seg[j].K for j in range(p.nseg)) >= int(os.environ.get("SCA_NTB_MIN_K", "1024"))
+                for p in chunk):
+        t = 41  # gemm.hip gemm_impl: the big NT / NN GEMMs
     a_kc, b_kc = layout != L.GEMM_TN, layout == L.GEMM_NT
     segs = [(p, p.seg[j]) for p in chunk for j in range(p.nseg)]
     vec = all(not ((a_kc or b_kc) and g.K % 4) and g.lda % 4 == 0 and g.ldb % 4 == 0 and (g.A or 0) % 16 == 0
@@ -211,6 +216,12 @@ def _gemm_kernel_name(layout, chunk, tile):
         return f"gemm_kernel<{layout}, T1, false>"
     glds = all(p.M % 4 == 0 and p.N % 4 == 0 for p in chunk) and \
         all(g.K % 32 == 0 and g.alpha == p.seg[0].alpha for p, g in segs)
+    if t in (41, 42):
+        if layout != L.GEMM_TN and glds and splitk == 1 and all(p.seg[j].K % 64 == 0 and p.seg[j].K > 0
+                                                                for p in chunk for j in range(p.nseg)):
+            return {41: "gemm_ntb_kernel<true, 6, %s>", 42: "gemm_ntb_kernel<false, 2, %s>"}[t] % \
+                str(layout == L.GEMM_NN).lower()
+        t = 20 if layout == L.GEMM_NT else 21
     if t in (38, 39, 40):
         if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
             return {38: "gemm_tnb_kernel<false, 2>", 39: "gemm_tnb_kernel<true, 4>", 40: "gemm_tnb_kernel<true, 6>"}[t]
@@ -234,7 +245,7 @@ def gemm(layout, probs, splitk=1, ws=None, tile=0):
         chunk = probs[i:i + L.GEMM_MAX_PROBLEMS]
         arr = (L.GemmProblem * len(chunk))(*chunk)
         flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in chunk for j in range(p.nseg)) if _PROFILER else 0.0
-        kname = _gemm_kernel_name(layout, chunk, tile) if _PROFILER else ""
+        kname = _gemm_kernel_name(layout, chunk, tile, splitk) if _PROFILER else ""
         if splitk > 1 and _SPLITK_FUSED and "sca_gemm_splitk_fused" not in L.MISSING:
             cnt = _splitk_counters(lib.sca_gemm_splitk_counters(len(chunk), max(p.M for p in chunk),
                                                                 max(p.N for p in chunk)),

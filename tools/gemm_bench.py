@@ -13,7 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4"}
+TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4", 41: "NTB128i", 42: "NTB128"}
 
 
 def make_case(name, layout, shapes, splitk=1, segs=1):
@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--tiles", default="", help="comma-separated tile ids")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--kscan", action="store_true", help="fixed-cost probe: NT 4x/12x(2048,256,K) over K")
+    ap.add_argument("--cfg5", action="store_true", help="config 5's NT / NN shapes (B x T = 8192 rows, d 512)")
     args = ap.parse_args()
     if args.lib:
         L.LIB_PATH = os.path.abspath(args.lib)
@@ -85,6 +86,14 @@ def main():
         make_case("NT longK 4x(2048,256,4096)", L.GEMM_NT, [(M, d, 4096)] * 4),
         make_case("NT longK 12x(2048,256,2048)", L.GEMM_NT, [(M, d, 2048)] * 12),
     ]
+    if args.cfg5:
+        M5, d5, F5 = 8192, 512, 1536
+        cases = [make_case("NT5 qkv 12x(8192,512,512)", L.GEMM_NT, [(M5, d5, d5)] * 12),
+                 make_case("NT5 ffn1 4x(8192,1536,512)", L.GEMM_NT, [(M5, F5, d5)] * 4),
+                 make_case("NT5 ffn2 4x(8192,512,1536)", L.GEMM_NT, [(M5, d5, F5)] * 4),
+                 make_case("NN5 dffn1 4x(8192,512,1536)", L.GEMM_NN, [(M5, d5, F5)] * 4),
+                 make_case("NN5 dffn2 4x(8192,1536,512)", L.GEMM_NN, [(M5, F5, d5)] * 4),
+                 make_case("NN5 dx-qkv 4x(8192,512,3x512)", L.GEMM_NN, [(M5, d5, d5)] * 4, segs=3)] + cases
     if args.kscan:
         cases = [make_case(f"NT kscan {n}x(2048,256,{k})", L.GEMM_NT, [(M, d, k)] * n)
                  for n in (4, 12) for k in (32, 64, 128, 256, 512, 1024)]
@@ -95,9 +104,14 @@ def main():
             if str(k) not in args.tiles.split(","):
                 del TILES[k]
     lib = L.lib()
+
+    def valid(layout, t):  # variant ids of one layout only (41 / 42: NT) are skipped elsewhere
+        return lib.sca_gemm_tile_override(layout, t) == 0
+
     for c in cases:
         for t in TILES:
-            lib.sca_gemm_tile_override(c["layout"], t)
+            if not valid(c["layout"], t):
+                continue
             ops.gemm(c["layout"], c["probs"], c["splitk"], c["ws"])
             torch.cuda.synchronize()
             for C, ref in ([] if args.no_check else c["refs"]):
@@ -108,7 +122,8 @@ def main():
     graphs = {}
     for c in cases:  # capture `iters` launches per (case, tile): times the GPU, not the Python launcher
         for t in TILES:
-            lib.sca_gemm_tile_override(c["layout"], t)
+            if not valid(c["layout"], t):
+                continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(args.iters):
@@ -117,7 +132,9 @@ def main():
     for rnd in range(args.rounds):
         for c in cases:
             for t in TILES:
-                g = graphs[(c["name"], t)]
+                g = graphs.get((c["name"], t))
+                if g is None:
+                    continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 g.replay()
@@ -126,7 +143,8 @@ def main():
                 tf = c["flops"] * args.iters / (e0.elapsed_time(e1) / 1e3) / 1e12
                 res.setdefault((c["name"], t), []).append(tf)
     for c in cases:
-        print(f"{c['name']:34s} " + " ".join(f"{max(res[(c['name'], t)]):9.1f}" for t in TILES))
+        print(f"{c['name']:34s} " + " ".join(f"{max(res[(c['name'], t)]):9.1f}" if (c['name'], t) in res
+                                              else f"{'-':>9s}" for t in TILES))
     for lay in range(3):
         lib.sca_gemm_tile_override(lay, 0)
 
