@@ -991,6 +991,29 @@ __device__ __forceinline__ void epilogue_piece(const sca_gemm_problem& P, f32x4 
   st4(P.C + (long)m * P.ldc + n, o + ex);
 }
 
+// Instruction interleave for the register-staged kernels' two phases (sched_group_barrier masks:
+// 0x008 MFMA, 0x020 VMEM read, 0x100 DS read, 0x200 DS write): the store phase as R rounds of
+// {W DS writes, 1 buffer load, M MFMAs} and the read phase as R rounds of {D DS reads, M MFMAs}
+// (hipBLASLt's MT128x128x64 fp32 kernel spreads them the same way: a burst of 16 loads or
+// writes stalls the issuing wave on the memory queues while the MFMA pipe idles)
+template <int I, int R, int W, int M>
+__device__ __forceinline__ void ilv_store() {
+  if constexpr (I < R) {
+    __builtin_amdgcn_sched_group_barrier(0x200, W, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
+    ilv_store<I + 1, R, W, M>();
+  }
+}
+template <int I, int R, int D, int M>
+__device__ __forceinline__ void ilv_read() {
+  if constexpr (I < R) {
+    __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
+    ilv_read<I + 1, R, D, M>();
+  }
+}
+
 __device__ __forceinline__ f32x4 tb_load(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
   return *reinterpret_cast<const f32x4*>(&r);
@@ -1000,7 +1023,7 @@ __device__ __forceinline__ f32x4 tb_load(__amdgpu_buffer_rsrc_t rs, int voff, in
 // store / load phase at one workgroup per CU, those of 0 .. NPRE-1 the fragment reads); else
 // the compiler's order (every MFMA between the fragment reads, ~216 registers: two workgroups
 // per CU cover each other's phases)
-template <bool INTER, int NPRE>
+template <bool INTER, int NPRE, bool ILV = false>
 __global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) float lds[2 * TB_OP];
   __shared__ unsigned flag;
@@ -1081,6 +1104,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[n][i], b[n][j], acc[i][j]);
+    if constexpr (ILV) ilv_read<0, 8, 4, 2 * NPRE>();
     if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
@@ -1094,6 +1118,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[n][i], b[n][j], acc[i][j]);
+    if constexpr (ILV && WR) ilv_store<0, 16, 1, (16 - NPRE)>();
     if (do_bias) {
 #pragma unroll
       for (int n = 0; n < 16; ++n) bs4 += a[n];
@@ -1213,7 +1238,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
 constexpr int NB_LD = TB_BK + 4;               // 68
 constexpr int NB_OP = TB_BM * NB_LD;           // floats per operand image
 
-template <bool INTER, int NPRE, bool B_KN>
+template <bool INTER, int NPRE, bool B_KN, bool ILV = false>
 __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) float lds[2 * NB_OP];
 
@@ -1310,6 +1335,7 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
           for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[t >> 2][i][t & 3], b[t >> 2][j][t & 3], acc[i][j]);
     };
     steps(0, NPRE);
+    if constexpr (ILV) ilv_read<0, 8, 4, 2 * NPRE>();
     if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
@@ -1318,6 +1344,7 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
       if constexpr (LD) load(it + 2);
     }
     steps(NPRE, 16);
+    if constexpr (ILV && WR) ilv_store<0, 16, B_KN ? 3 : 1, (16 - NPRE)>();
     __syncthreads();
   };
   load(0);
@@ -2129,6 +2156,7 @@ int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
 //   36 / 37  TN only: the k-split outer-product weight-gradient kernel, 3- / 4-stage ring
 //   38 / 39 / 40  TN only: 128x128 tiles, register-staged operand stream (gemm_tnb_kernel<INTER, NPRE>)
 //   41 / 42  NT / NN: the same with A k-contiguous (gemm_ntb_kernel<INTER, NPRE, B k-major>)
+//   43 / 44  TN / NT-NN: variants 40 / 41 with the phases' instructions interleaved (ILV)
 using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
 using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
 using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
@@ -2137,8 +2165,8 @@ constexpr int kTnFirst = 36, kTnLast = 40;
 bool valid_tile(int layout, int tile) {
   switch (tile) {
     case 0: case 1: case 5: case 7: case 20: case 21: case 22: return true;
-    case 36: case 37: case 38: case 39: case 40: return layout == SCA_GEMM_TN;
-    case 41: case 42: return layout != SCA_GEMM_TN;
+    case 36: case 37: case 38: case 39: case 40: case 43: return layout == SCA_GEMM_TN;
+    case 41: case 42: case 44: return layout != SCA_GEMM_TN;
     default: return false;
   }
 }
@@ -2220,32 +2248,35 @@ bool ntb_ok(const GemmArgs& a, int nprob, bool b_kn) {
   return true;
 }
 
-template <bool INTER, int NPRE, bool B_KN>
+template <bool INTER, int NPRE, bool B_KN, bool ILV = false>
 int launch_ntb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + TB_BM - 1) / TB_BM, (maxM + TB_BM - 1) / TB_BM, nprob);
-  hipLaunchKernelGGL((gemm_ntb_kernel<INTER, NPRE, B_KN>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((gemm_ntb_kernel<INTER, NPRE, B_KN, ILV>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-template <bool INTER, int NPRE>
+template <bool INTER, int NPRE, bool ILV = false>
 int launch_tnb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + TB_BM - 1) / TB_BM, (maxM + TB_BM - 1) / TB_BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_tnb_kernel<INTER, NPRE>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((gemm_tnb_kernel<INTER, NPRE, ILV>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
-  if (tile == 41 || tile == 42) {
+  if (tile == 41 || tile == 42 || tile == 44) {
     constexpr bool KN = LAYOUT == SCA_GEMM_NN;
-    if (LAYOUT != SCA_GEMM_TN && ntb_ok(a, nprob, KN))
+    if (LAYOUT != SCA_GEMM_TN && ntb_ok(a, nprob, KN)) {
+      if (tile == 44) return launch_ntb<true, 6, KN, true>(a, nprob, maxM, maxN, st);
       return tile == 41 ? launch_ntb<true, 6, KN>(a, nprob, maxM, maxN, st)
                         : launch_ntb<false, 2, KN>(a, nprob, maxM, maxN, st);
+    }
     tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;
   }
-  if (tile >= 38 && tile <= 40) {
+  if ((tile >= 38 && tile <= 40) || tile == 43) {
     if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) {
+      if (tile == 43) return launch_tnb<true, 6, true>(a, nprob, maxM, maxN, st);
       if (tile == 38) return launch_tnb<false, 2>(a, nprob, maxM, maxN, st);
       return tile == 39 ? launch_tnb<true, 4>(a, nprob, maxM, maxN, st) : launch_tnb<true, 6>(a, nprob, maxM, maxN, st);
     }
@@ -2276,7 +2307,7 @@ bool ntb_default() {
   return on;
 }
 int ntb_min_k() {
-  static const int k = getenv("SCA_NTB_MIN_K") ? atoi(getenv("SCA_NTB_MIN_K")) : 1024;
+  static const int k = getenv("SCA_NTB_MIN_K") ? atoi(getenv("SCA_NTB_MIN_K")) : 512;
   return k;
 }
 
@@ -2400,10 +2431,10 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
       for (int s2 = 0; s2 < probs[i].nseg; ++s2) k += probs[i].seg[s2].K;
       longk = longk && k >= ntb_min_k();
     }
-    if (longk) tile = 41;
+    if (longk) tile = 44;
   }
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
-  const bool tn_big = layout == SCA_GEMM_TN && tile >= kTnFirst && tile <= kTnLast && tn_ok(a, nprob);
+  const bool tn_big = layout == SCA_GEMM_TN && ((tile >= kTnFirst && tile <= kTnLast) || tile == 43) && tn_ok(a, nprob);
   if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&
       vec_ok(a, nprob, layout)) {
     a.counters = counters;

@@ -205,9 +205,9 @@ def _gemm_kernel_name(layout, chunk, tile, splitk=1):
     t = tile or (20 if layout == L.GEMM_NT else 21)
     if not tile and layout != L.GEMM_TN and splitk == 1 and os.environ.get("SCA_NTB", "1") != "0" and \
             sum(-(-p.M // 64) * -(-p.N // 64) for p in chunk) >= 2048 and \
-            all(sum(p.seg[j].K for j in range(p.nseg)) >= int(os.environ.get("SCA_NTB_MIN_K", "1024"))
+            all(sum(p.seg[j].K for j in range(p.nseg)) >= int(os.environ.get("SCA_NTB_MIN_K", "512"))
                 for p in chunk):
-        t = 41  # gemm.hip gemm_impl: the big NT / NN GEMMs
+        t = 44  # gemm.hip gemm_impl: the big NT / NN GEMMs
     a_kc, b_kc = layout != L.GEMM_TN, layout == L.GEMM_NT
     segs = [(p, p.seg[j]) for p in chunk for j in range(p.nseg)]
     vec = all(not ((a_kc or b_kc) and g.K % 4) and g.lda % 4 == 0 and g.ldb % 4 == 0 and (g.A or 0) % 16 == 0
@@ -216,15 +216,16 @@ def _gemm_kernel_name(layout, chunk, tile, splitk=1):
         return f"gemm_kernel<{layout}, T1, false>"
     glds = all(p.M % 4 == 0 and p.N % 4 == 0 for p in chunk) and \
         all(g.K % 32 == 0 and g.alpha == p.seg[0].alpha for p, g in segs)
-    if t in (41, 42):
+    if t in (41, 42, 44):
         if layout != L.GEMM_TN and glds and splitk == 1 and all(p.seg[j].K % 64 == 0 and p.seg[j].K > 0
                                                                 for p in chunk for j in range(p.nseg)):
-            return {41: "gemm_ntb_kernel<true, 6, %s>", 42: "gemm_ntb_kernel<false, 2, %s>"}[t] % \
-                str(layout == L.GEMM_NN).lower()
+            return {41: "gemm_ntb_kernel<true, 6, %s, false>", 42: "gemm_ntb_kernel<false, 2, %s, false>",
+                    44: "gemm_ntb_kernel<true, 6, %s, true>"}[t] % str(layout == L.GEMM_NN).lower()
         t = 20 if layout == L.GEMM_NT else 21
-    if t in (38, 39, 40):
+    if t in (38, 39, 40, 43):
         if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
-            return {38: "gemm_tnb_kernel<false, 2>", 39: "gemm_tnb_kernel<true, 4>", 40: "gemm_tnb_kernel<true, 6>"}[t]
+            return {38: "gemm_tnb_kernel<false, 2, false>", 39: "gemm_tnb_kernel<true, 4, false>",
+                    40: "gemm_tnb_kernel<true, 6, false>", 43: "gemm_tnb_kernel<true, 6, true>"}[t]
         t = 36
     if t in _TILE_NAMES:
         if layout == L.GEMM_TN and glds and all(p.nseg == 1 for p in chunk):
@@ -610,15 +611,16 @@ _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per
 _TNK_TILES_PER_PROBLEM = 48
 
 
-# the 128x128 register-staged weight-gradient kernel (tile 40) for long reductions (config 5:
-# K = 8192 rows); measured with tools/tn_library_compare.py: 0.82 of peak with
-# two workgroups per CU, 0.72 with one, against the k-split kernel's 0.72-0.74
+# the 128x128 register-staged weight-gradient kernel with interleaved phases (tile 43) for long
+# reductions (config 5: K = 8192 rows); measured with tools/tn_library_compare.py (DESIGN.md
+# §9R.1): 0.88 of peak with one workgroup per CU, 0.86 with two, against the k-split kernel's
+# 0.74; at config 2 / 3's K <= 2048 it has too few tiles and loses
 _TNB_MIN_K = int(os.environ.get("SCA_TNB_MIN_K", "4096"))  # A/B switch (0: never)
-_TNB_RATE2, _TNB_RATE1, _TNB_EPI = 0.81, 0.72, 3.0
+_TNB_RATE2, _TNB_RATE1, _TNB_EPI = 0.86, 0.88, 3.0
 
 
 def _tnb_split(K, tiles128):
-    """Split-K for tile 40: the split whose estimated per-CU time is least — workgroups dealt
+    """Split-K for tile 43: the split whose estimated per-CU time is least — workgroups dealt
     over 256 CUs, two at a time at _TNB_RATE2, a leftover one at _TNB_RATE1, plus an epilogue
     cost per workgroup (ties: the smaller split, fewer slabs)."""
     best, best_sk = None, 1
@@ -899,7 +901,7 @@ def _weight_grads(items):
             tile = 0
             Kr = items[sub[0]][0].shape[0]
             if 0 < _TNB_MIN_K <= Kr and Kr % 64 == 0:
-                tile = 40
+                tile = 43
                 sk = _tnb_split(Kr, sum(-(-items[i][3].shape[0] // 128) * -(-items[i][3].shape[1] // 128)
                                         for i in sub))
             elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):

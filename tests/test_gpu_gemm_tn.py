@@ -53,7 +53,7 @@ def _check(items, alpha=1.0, bscale=1.0, base=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 37, 38, 39, 40])
+@pytest.mark.parametrize("tile", [36, 37, 38, 39, 40, 43])
 @pytest.mark.parametrize("splitk,fused", [(1, False), (2, False), (2, True), (3, True), (5, True)])
 def test_ksplit_kernel_matches_float64(tile, splitk, fused):
     """gemm_tnk_kernel (tiles 36 / 37) and gemm_tnb_kernel (38): M not a multiple of 64 / 128,
@@ -105,7 +105,7 @@ def test_tnb_tile_falls_back_when_k_is_not_a_multiple_of_64():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 38, 39])
+@pytest.mark.parametrize("tile", [36, 38, 39, 43])
 def test_ksplit_bias_off_and_accumulate(tile):
     items = _case([(128, 192)] * 3, 512, seed=5, bias=False)
     base = [torch.randn(128, 192, device="cuda") for _ in items]
@@ -116,7 +116,7 @@ def test_ksplit_bias_off_and_accumulate(tile):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 38, 39])
+@pytest.mark.parametrize("tile", [36, 38, 39, 43])
 def test_ksplit_is_deterministic(tile):
     """The split-K slabs are summed in slice order whichever split arrives last."""
     items = _case([(256, 256)] * 6, 2048, seed=9)

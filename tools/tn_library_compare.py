@@ -17,6 +17,7 @@ from scattennet_amd import _lib as L, ops  # noqa: E402
 
 PEAK = 157.3
 SPLITS = (1, 2, 3, 4, 5, 6, 8)  # --splits
+TNB_TILES = (38, 39, 40, 43)  # --tnb-tiles
 LIBRARY = False  # --library: the hipBLASLt timings only, eagerly, in a process that captures no graph
 
 
@@ -46,7 +47,7 @@ def variants(c):
         if c["K"] // sk < 256 and sk > 1:
             continue
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
-        for tl in (38, 39, 40):
+        for tl in TNB_TILES:
             out.append((f"tnb{tl} sk={sk} wg={t128 * sk}", lambda sk=sk, ws=ws, tl=tl: ops.gemm(
                 L.GEMM_TN, P, splitk=sk, ws=ws, tile=tl)))
     if LIBRARY and len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
@@ -71,9 +72,11 @@ def main():
                                                    "--iters times each, for rocprofv3 counter passes "
                                                    "(tools/tn_pmc2.py)")
     ap.add_argument("--splits", default="1,2,3,4,5,6,8", help="split-K values of the 128x128 kernels")
+    ap.add_argument("--tnb-tiles", default="38,39,40,43", help="variant ids of the 128x128 kernel")
     args = ap.parse_args()
-    global LIBRARY, SPLITS
+    global LIBRARY, SPLITS, TNB_TILES
     SPLITS = tuple(int(x) for x in args.splits.split(","))
+    TNB_TILES = tuple(int(x) for x in args.tnb_tiles.split(","))
     LIBRARY = args.library
     torch.manual_seed(0)
     cases = [case("cfg2 attn 16x(256,256)", [(256, 256)] * 16, 2048),
