@@ -713,6 +713,38 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const GemmArgs args) {
   SCA_STAMP(3);
 }
 
+constexpr int TB_BM = 128, TB_BK = 64;
+constexpr int TB_OP = TB_BK * TB_BM;  // floats per operand tile (32 KB)
+
+
+// Instruction interleave for the register-staged kernels' two phases (sched_group_barrier masks:
+// 0x008 MFMA, 0x020 VMEM read, 0x100 DS read, 0x200 DS write): the store phase as R rounds of
+// {W DS writes, 1 buffer load, M MFMAs} and the read phase as R rounds of {D DS reads, M MFMAs}
+// (hipBLASLt's MT128x128x64 fp32 kernel spreads them the same way: a burst of 16 loads or
+// writes stalls the issuing wave on the memory queues while the MFMA pipe idles)
+template <int I, int R, int W, int M>
+__device__ __forceinline__ void ilv_store() {
+  if constexpr (I < R) {
+    __builtin_amdgcn_sched_group_barrier(0x200, W, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
+    ilv_store<I + 1, R, W, M>();
+  }
+}
+template <int I, int R, int D, int M>
+__device__ __forceinline__ void ilv_read() {
+  if constexpr (I < R) {
+    __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
+    ilv_read<I + 1, R, D, M>();
+  }
+}
+
+__device__ __forceinline__ f32x4 tb_load(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  return *reinterpret_cast<const f32x4*>(&r);
+}
+
 // ------------------------------------------------------------------------------ TN, k-split waves
 // Weight-gradient GEMM (TN: dW[M x N] = A^T B over K rows; A = dY [K][M], B = X [K][N], both
 // k-major, the LDS-DMA ring of gemm_glds_kernel) with 16x16x4 MFMAs in an outer-product form:
@@ -730,8 +762,11 @@ constexpr int TNK_PLD = 68;  // partial-tile row stride (floats): 16-B shift per
 // 48-KB ring and three workgroups share a CU (the one-round form took 70 KB: two per CU)
 constexpr int TNK_RED = 2 * 64 * TNK_PLD * 4 + 4 * 64 * 4;
 
-// SUB: K slices per ring stage (one wait + barrier per SUB x 32 k rows)
-template <int S, int SUB>
+// SUB: K slices per ring stage (one wait + barrier per SUB x 32 k rows).  REG: the operand
+// stream of gemm_tnb_kernel instead of the LDS-DMA ring — 64 k rows per iteration (wave w
+// takes rows 16w .. 16w+15), the next iteration's pieces register-staged (4 + 4 float4 per
+// thread), loads / stores / fragment reads interleaved with the MFMAs; one segment, K % 64 == 0
+template <int S, int SUB, bool REG = false>
 __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   constexpr int SLICE = 2 * GL_OP_BYTES;
   constexpr int STAGE = SUB * SLICE;
@@ -813,6 +848,84 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (REG) {
+    const sca_gemm_seg& G = P.seg[0];
+    const int K = G.K;
+    const int chunk = ((K + splitk - 1) / splitk + TB_BK - 1) / TB_BK * TB_BK;
+    const int kbeg = min(K, ks * chunk), kend = min(K, kbeg + chunk);
+    const int nit = (kend - kbeg) / TB_BK;
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.A), 0, (int)(((long)(K - 1) * G.lda + P.M) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.B), 0, (int)(((long)(K - 1) * G.ldb + P.N) * 4), 0x00020000);
+    // thread's pieces j < 4: k row (tid >> 4) + 16j of the iteration, columns 4 (tid & 15) .. +3
+    const int tid = threadIdx.x, srow = tid >> 4, scol = 4 * (tid & 15);
+    const int va = (int)(((long)(kbeg + srow) * G.lda + min(m0 + scol, P.M - 4)) * 4);
+    const int vb = (int)(((long)(kbeg + srow) * G.ldb + min(n0 + scol, P.N - 4)) * 4);
+    const int rowA = 16 * G.lda * 4, rowB = 16 * G.ldb * 4, itA = TB_BK * G.lda * 4, itB = TB_BK * G.ldb * 4;
+    float* As = reinterpret_cast<float*>(smem);  // [64 k][64 m], then [64 k][64 n]
+    float* Bs = As + TB_BK * GL_BM;
+    f32x4 st[8];
+    auto load = [&](int it) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st[j] = tb_load(ra, va, it * itA + j * rowA);
+        st[4 + j] = tb_load(rb, vb, it * itB + j * rowB);
+      }
+    };
+    auto store = [&]() {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st4(As + (srow + 16 * j) * GL_BM + scol, st[j]);
+        st4(Bs + (srow + 16 * j) * GL_BN + scol, st[4 + j]);
+      }
+    };
+    auto iter = [&](auto wr_c, auto ld_c, int it) {
+      constexpr bool WR = decltype(wr_c)::value, LD = decltype(ld_c)::value;
+      f32x4 a[4], b[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int k = 16 * wave + 4 * n + g;
+        a[n] = ld4(As + k * GL_BM + 4 * c);
+        b[n] = ld4(Bs + k * GL_BN + 4 * c);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[0][i], b[0][j], acc[i][j]);
+      ilv_read<0, 2, 4, 8>();
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (WR) {
+        store();
+        if constexpr (LD) load(it + 2);
+      }
+#pragma unroll
+      for (int n = 1; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[n][i], b[n][j], acc[i][j]);
+      if constexpr (WR) ilv_store<0, 8, 1, 6>();
+      if (do_bias) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bs4 += a[n];
+      }
+      __syncthreads();
+    };
+    if (nit > 0) {
+      load(0);
+      store();
+      if (nit > 1) load(1);
+      __syncthreads();
+    }
+    int it = 0;
+#pragma unroll 1
+    for (; it + 2 < nit; ++it) iter(std::true_type{}, std::true_type{}, it);
+    if (it + 1 < nit) iter(std::true_type{}, std::false_type{}, it++);
+    if (it < nit) iter(std::false_type{}, std::false_type{}, it);
+  } else {
 #pragma unroll
   for (int i = 0; i < S - 1; ++i)
     if (i < nst) dma_stage(i, i);
@@ -847,6 +960,7 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
       }
     }
   }
+  }  // REG
 
   // the 4 waves' partial tiles (and bias rows) through LDS, summed in a fixed order:
   // (wave 0 + wave 2) + (wave 1 + wave 3), in two rounds over two tile slots
@@ -963,9 +1077,6 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
 // wm + 16g + 4r + i (g = lane >> 4; r, i < 4) x columns wn + 4c .. 4c+3 (c = lane & 15), stored
 // as float4 row pieces straight from the accumulators.  Split-K: slabs + in-launch combine
 // (gemm_glds_kernel's protocol) or the separate reduction.  Requires K % 64 == 0 per problem.
-constexpr int TB_BM = 128, TB_BK = 64;
-constexpr int TB_OP = TB_BK * TB_BM;  // floats per operand tile (32 KB)
-
 // epilogue_rows' per-piece body: one float4 of row m at columns n .. n+3
 __device__ __forceinline__ void epilogue_piece(const sca_gemm_problem& P, f32x4 v, int m, int n,
                                                const DropMask& dm) {
@@ -991,33 +1102,6 @@ __device__ __forceinline__ void epilogue_piece(const sca_gemm_problem& P, f32x4 
   st4(P.C + (long)m * P.ldc + n, o + ex);
 }
 
-// Instruction interleave for the register-staged kernels' two phases (sched_group_barrier masks:
-// 0x008 MFMA, 0x020 VMEM read, 0x100 DS read, 0x200 DS write): the store phase as R rounds of
-// {W DS writes, 1 buffer load, M MFMAs} and the read phase as R rounds of {D DS reads, M MFMAs}
-// (hipBLASLt's MT128x128x64 fp32 kernel spreads them the same way: a burst of 16 loads or
-// writes stalls the issuing wave on the memory queues while the MFMA pipe idles)
-template <int I, int R, int W, int M>
-__device__ __forceinline__ void ilv_store() {
-  if constexpr (I < R) {
-    __builtin_amdgcn_sched_group_barrier(0x200, W, 0);
-    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
-    ilv_store<I + 1, R, W, M>();
-  }
-}
-template <int I, int R, int D, int M>
-__device__ __forceinline__ void ilv_read() {
-  if constexpr (I < R) {
-    __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
-    ilv_read<I + 1, R, D, M>();
-  }
-}
-
-__device__ __forceinline__ f32x4 tb_load(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
-  return *reinterpret_cast<const f32x4*>(&r);
-}
 
 // INTER: the MFMAs of k-steps NPRE .. 15 pinned after the staged-piece stores (they cover the
 // store / load phase at one workgroup per CU, those of 0 .. NPRE-1 the fragment reads); else
@@ -1238,9 +1322,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tnb_kernel(const GemmArgs args) {
 constexpr int NB_LD = TB_BK + 4;               // 68
 constexpr int NB_OP = TB_BM * NB_LD;           // floats per operand image
 
-template <bool INTER, int NPRE, bool B_KN, bool ILV = false>
+template <bool INTER, int NPRE, bool B_KN, bool ILV = false, int TM = 128>
 __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * NB_OP];
+  constexpr int WT = TM / 2, NQ = WT / 16, NJ = TM / 16;  // wave tile, its 16-blocks, pieces / operand
+  constexpr int OP = TM * NB_LD;                            // floats per operand image
+  __shared__ __attribute__((aligned(16))) float lds[2 * OP];
+  if constexpr (B_KN && SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);  // as gemm_glds_kernel<NN>
 
   const unsigned gx = gridDim.x, gy = gridDim.y;
   const unsigned nwg = gx * gy * gridDim.z;
@@ -1249,21 +1336,21 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
   const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int bx = wgid % gx, by = (wgid / gx) % gy, pid = wgid / (gx * gy);
   const sca_gemm_problem& P = args.p[pid];
-  const int m0 = by * TB_BM, n0 = bx * TB_BM;
+  const int m0 = by * TM, n0 = bx * TM;
   if (m0 >= P.M || n0 >= P.N) return;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = lane >> 4, li = lane & 15;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave >> 1) * WT, wn = (wave & 1) * WT;
   const int nseg = P.nseg;
   const int it0 = P.seg[0].K / TB_BK, it1 = nseg > 1 ? P.seg[1].K / TB_BK : 0;
   const int nit = it0 + it1 + (nseg > 2 ? P.seg[2].K / TB_BK : 0);
 
-  // thread's staged pieces j < 8: A (and NT's B) row (tid >> 4) + 16j, k 4 (tid & 15) .. +3 of
+  // thread's staged pieces j < NJ: A (and NT's B) row (tid >> 4) + 16j, k 4 (tid & 15) .. +3 of
   // the iteration; NN's B: k 16 (b & 3) + (lane & 15), columns 4 (4 (b >> 2) + (lane >> 4)) ..
-  // +3 with b = 8 wave + j.  Rows / columns past the end re-read the last ones (never stored).
+  // +3 with b = NJ wave + j.  Rows / columns past the end re-read the last ones (never stored).
   const int srow = tid >> 4, sk4 = 4 * (tid & 15);
-  f32x4 st[16];
+  f32x4 st[2 * NJ];
   auto load = [&](int it) {
     int s = 0, lit = it;  // segment and its local iteration (wave-uniform)
     if (lit >= it0) {
@@ -1281,48 +1368,48 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
         const_cast<float*>(G.B), 0,
         (int)((B_KN ? (long)(G.K - 1) * G.ldb + P.N : (long)(P.N - 1) * G.ldb + G.K) * 4), 0x00020000);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       st[j] = tb_load(ra, (int)(((long)min(m0 + srow + 16 * j, P.M - 1) * G.lda + sk4) * 4), lit * TB_BK * 4);
       if constexpr (B_KN) {
-        const int b = 8 * wave + j;
+        const int b = NJ * wave + j;
         const int k = 16 * (b & 3) + li, c4 = 4 * (4 * (b >> 2) + kg);
-        st[8 + j] = tb_load(rb, (int)(((long)k * G.ldb + min(n0 + c4, P.N - 4)) * 4), lit * TB_BK * G.ldb * 4);
+        st[NJ + j] = tb_load(rb, (int)(((long)k * G.ldb + min(n0 + c4, P.N - 4)) * 4), lit * TB_BK * G.ldb * 4);
       } else {
-        st[8 + j] = tb_load(rb, (int)(((long)min(n0 + srow + 16 * j, P.N - 1) * G.ldb + sk4) * 4), lit * TB_BK * 4);
+        st[NJ + j] = tb_load(rb, (int)(((long)min(n0 + srow + 16 * j, P.N - 1) * G.ldb + sk4) * 4), lit * TB_BK * 4);
       }
     }
   };
   float* wbase = lds + srow * NB_LD + sk4;
   auto store = [&]() {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       st4(wbase + j * 16 * NB_LD, st[j]);
       if constexpr (B_KN) {
-        const int b = 8 * wave + j;
+        const int b = NJ * wave + j;
         const int k = 16 * (b & 3) + li, c4 = 4 * (4 * (b >> 2) + kg);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) lds[NB_OP + (c4 + q) * NB_LD + k] = st[8 + j][q];
+        for (int q = 0; q < 4; ++q) lds[OP + (c4 + q) * NB_LD + k] = st[NJ + j][q];
       } else {
-        st4(wbase + NB_OP + j * 16 * NB_LD, st[8 + j]);
+        st4(wbase + OP + j * 16 * NB_LD, st[NJ + j]);
       }
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[NQ][NQ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NQ; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NQ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const float* ra_lds = lds + (wm + li) * NB_LD + 4 * kg;
-  const float* rb_lds = lds + NB_OP + (wn + li) * NB_LD + 4 * kg;
+  const float* rb_lds = lds + OP + (wn + li) * NB_LD + 4 * kg;
   auto iter = [&](auto wr_c, auto ld_c, int it) {
     constexpr bool WR = decltype(wr_c)::value, LD = decltype(ld_c)::value;
-    f32x4 a[4][4], b[4][4];  // [kc][block]
+    f32x4 a[4][NQ], b[4][NQ];  // [kc][block]
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         a[kc][q] = ld4(ra_lds + 16 * q * NB_LD + 16 * kc);
         b[kc][q] = ld4(rb_lds + 16 * q * NB_LD + 16 * kc);
       }
@@ -1330,12 +1417,12 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
 #pragma unroll
       for (int t = t0; t < t1; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NQ; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[t >> 2][i][t & 3], b[t >> 2][j][t & 3], acc[i][j]);
+          for (int j = 0; j < NQ; ++j) acc[i][j] = mfma16(a[t >> 2][i][t & 3], b[t >> 2][j][t & 3], acc[i][j]);
     };
     steps(0, NPRE);
-    if constexpr (ILV) ilv_read<0, 8, 4, 2 * NPRE>();
+    if constexpr (ILV) ilv_read<0, 8, NQ, NPRE * NQ * NQ / 8>();
     if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     if constexpr (INTER) __builtin_amdgcn_sched_barrier(0);
@@ -1344,7 +1431,7 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
       if constexpr (LD) load(it + 2);
     }
     steps(NPRE, 16);
-    if constexpr (ILV && WR) ilv_store<0, 16, B_KN ? 3 : 1, (16 - NPRE)>();
+    if constexpr (ILV && WR) ilv_store<0, 2 * NJ, B_KN ? 3 : 1, (16 - NPRE) * NQ * NQ / (2 * NJ)>();
     __syncthreads();
   };
   load(0);
@@ -1357,26 +1444,28 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
   if (it + 1 < nit) iter(std::true_type{}, std::false_type{}, it++);
   if (it < nit) iter(std::false_type{}, std::false_type{}, it);
 
-  // accumulators -> this wave's 64 x 68 image -> float4 row pieces (rows kg + 4q, columns 4 li)
-  float* img = lds + wave * 64 * NB_LD;
+  // accumulators -> this wave's WT x 68 image -> float4 row pieces (LR lanes per row: rows
+  // lane / LR + (64 / LR) q, columns 4 (lane % LR))
+  constexpr int LR = WT / 4;
+  float* img = lds + wave * WT * NB_LD;
   const float alpha = P.seg[0].alpha;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NQ; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NQ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) img[(16 * i + 4 * kg + r) * NB_LD + 16 * j + li] = acc[i][j][r] * alpha;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int n = n0 + wn + 4 * li;
+  const int n = n0 + wn + 4 * (lane % LR);
   if (n >= P.N) return;
   DropMask dm;
   if (P.epi & SCA_EPI_DROPOUT) dm.init(P.drop_seed, P.drop_p, args.drop_off);
 #pragma unroll 4
-  for (int q = 0; q < 16; ++q) {
-    const int rho = kg + 4 * q, m = m0 + wm + rho;
-    if (m < P.M) epilogue_piece(P, ld4(img + rho * NB_LD + 4 * li), m, n, dm);
+  for (int q = 0; q < WT * LR / 64; ++q) {
+    const int rho = lane / LR + (64 / LR) * q, m = m0 + wm + rho;
+    if (m < P.M) epilogue_piece(P, ld4(img + rho * NB_LD + 4 * (lane % LR)), m, n, dm);
   }
 }
 
@@ -2157,6 +2246,8 @@ int launch(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
 //   38 / 39 / 40  TN only: 128x128 tiles, register-staged operand stream (gemm_tnb_kernel<INTER, NPRE>)
 //   41 / 42  NT / NN: the same with A k-contiguous (gemm_ntb_kernel<INTER, NPRE, B k-major>)
 //   43 / 44  TN / NT-NN: variants 40 / 41 with the phases' instructions interleaved (ILV)
+//   45  NT / NN: variant 44 on 64x64 tiles (4 waves of 32x32: four times the workgroups)
+//   46  TN: the k-split kernel (36) with the register-staged, interleaved operand stream
 using T1 = Cfg<64, 64, 2, 2, 32, 2>;    // 4 waves, 32x32 each, double-buffered
 using T5 = Cfg<64, 64, 2, 2, 32, 1>;    // single-buffered (more workgroups per CU)
 using T7 = Cfg<128, 64, 4, 2, 32, 2>;   // 8 waves, 32x32
@@ -2165,8 +2256,8 @@ constexpr int kTnFirst = 36, kTnLast = 40;
 bool valid_tile(int layout, int tile) {
   switch (tile) {
     case 0: case 1: case 5: case 7: case 20: case 21: case 22: return true;
-    case 36: case 37: case 38: case 39: case 40: case 43: return layout == SCA_GEMM_TN;
-    case 41: case 42: case 44: return layout != SCA_GEMM_TN;
+    case 36: case 37: case 38: case 39: case 40: case 43: case 46: return layout == SCA_GEMM_TN;
+    case 41: case 42: case 44: case 45: return layout != SCA_GEMM_TN;
     default: return false;
   }
 }
@@ -2203,10 +2294,10 @@ bool vec_ok(const GemmArgs& a, int nprob, int layout) {
   return true;
 }
 
-template <int S, int SUB>
+template <int S, int SUB, bool REG = false>
 int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
-  hipLaunchKernelGGL((gemm_tnk_kernel<S, SUB>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((gemm_tnk_kernel<S, SUB, REG>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -2248,10 +2339,10 @@ bool ntb_ok(const GemmArgs& a, int nprob, bool b_kn) {
   return true;
 }
 
-template <bool INTER, int NPRE, bool B_KN, bool ILV = false>
+template <bool INTER, int NPRE, bool B_KN, bool ILV = false, int TM = 128>
 int launch_ntb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  dim3 grid((maxN + TB_BM - 1) / TB_BM, (maxM + TB_BM - 1) / TB_BM, nprob);
-  hipLaunchKernelGGL((gemm_ntb_kernel<INTER, NPRE, B_KN, ILV>), grid, dim3(256), 0, st, a);
+  dim3 grid((maxN + TM - 1) / TM, (maxM + TM - 1) / TM, nprob);
+  hipLaunchKernelGGL((gemm_ntb_kernel<INTER, NPRE, B_KN, ILV, TM>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
@@ -2265,14 +2356,19 @@ int launch_tnb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
 template <int LAYOUT>
 int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
-  if (tile == 41 || tile == 42 || tile == 44) {
+  if (tile == 41 || tile == 42 || tile == 44 || tile == 45) {
     constexpr bool KN = LAYOUT == SCA_GEMM_NN;
     if (LAYOUT != SCA_GEMM_TN && ntb_ok(a, nprob, KN)) {
+      if (tile == 45) return launch_ntb<true, 6, KN, true, 64>(a, nprob, maxM, maxN, st);
       if (tile == 44) return launch_ntb<true, 6, KN, true>(a, nprob, maxM, maxN, st);
       return tile == 41 ? launch_ntb<true, 6, KN>(a, nprob, maxM, maxN, st)
                         : launch_ntb<false, 2, KN>(a, nprob, maxM, maxN, st);
     }
     tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;
+  }
+  if (tile == 46) {
+    if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) return launch_tnk<3, 1, true>(a, nprob, maxM, maxN, st);
+    tile = 36;
   }
   if ((tile >= 38 && tile <= 40) || tile == 43) {
     if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) {
@@ -2433,8 +2529,13 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
     }
     if (longk) tile = 44;
   }
+  if (!variant && !g_tile_override[layout] && layout != SCA_GEMM_TN && splitk == 1 && tile != 44 &&
+      ntb_default())
+    tile = 45;  // every other NT / NN GEMM: the 64x64 form (tools/gemm_bench.py: +5 to +13 % over the
+                // LDS-DMA kernels at config 2's shapes); launch_tile hands ineligible shapes back
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
-  const bool tn_big = layout == SCA_GEMM_TN && ((tile >= kTnFirst && tile <= kTnLast) || tile == 43) && tn_ok(a, nprob);
+  const bool tn_big =
+      layout == SCA_GEMM_TN && ((tile >= kTnFirst && tile <= kTnLast) || tile == 43 || tile == 46) && tn_ok(a, nprob);
   if (counters && splitk > 1 && (tile == 20 || tile == 21 || tile == 22 || tn_big) && glds_ok(a, nprob) &&
       vec_ok(a, nprob, layout)) {
     a.counters = counters;

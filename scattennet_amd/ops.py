@@ -74,6 +74,10 @@ class _timed:
 
 # name prefixes of every kernel that can run a layout's plain GEMM (tests count launches by them)
 GEMM_KERNELS = {lay: (f"gemm_glds_kernel<{lay},", f"gemm_kernel<{lay}") for lay in range(3)}
+# the register-staged kernels (_gemm_kernel_name): NT / NN by their B-layout flag, TN by family
+GEMM_KERNELS[0] += ("gemm_ntb_kernel<true, 6, false", "gemm_ntb_kernel<false, 2, false")
+GEMM_KERNELS[1] += ("gemm_ntb_kernel<true, 6, true", "gemm_ntb_kernel<false, 2, true")
+GEMM_KERNELS[2] += ("gemm_tnk_kernel<", "gemm_tnb_kernel<")
 
 # rocprof names of the default (LDS-DMA) kernel per layout (gemm_glds_kernel<LAYOUT, STAGES>:
 # the ring depth pick_tile chooses, 3 stages forward, 2 for the gradient layouts)
@@ -195,7 +199,7 @@ def _splitk_counters(n, device=None):
     return ring[pos:pos + n]
 
 
-_TILE_NAMES = {36: "gemm_tnk_kernel<3, 1>", 37: "gemm_tnk_kernel<4, 1>"}
+_TILE_NAMES = {36: "gemm_tnk_kernel<3, 1, false>", 37: "gemm_tnk_kernel<4, 1, false>"}
 
 
 def _gemm_kernel_name(layout, chunk, tile, splitk=1):
@@ -208,6 +212,8 @@ def _gemm_kernel_name(layout, chunk, tile, splitk=1):
             all(sum(p.seg[j].K for j in range(p.nseg)) >= int(os.environ.get("SCA_NTB_MIN_K", "512"))
                 for p in chunk):
         t = 44  # gemm.hip gemm_impl: the big NT / NN GEMMs
+    elif not tile and layout != L.GEMM_TN and splitk == 1 and os.environ.get("SCA_NTB", "1") != "0":
+        t = 45  # the 64x64 form for the others
     a_kc, b_kc = layout != L.GEMM_TN, layout == L.GEMM_NT
     segs = [(p, p.seg[j]) for p in chunk for j in range(p.nseg)]
     vec = all(not ((a_kc or b_kc) and g.K % 4) and g.lda % 4 == 0 and g.ldb % 4 == 0 and (g.A or 0) % 16 == 0
@@ -216,12 +222,17 @@ def _gemm_kernel_name(layout, chunk, tile, splitk=1):
         return f"gemm_kernel<{layout}, T1, false>"
     glds = all(p.M % 4 == 0 and p.N % 4 == 0 for p in chunk) and \
         all(g.K % 32 == 0 and g.alpha == p.seg[0].alpha for p, g in segs)
-    if t in (41, 42, 44):
+    if t in (41, 42, 44, 45):
         if layout != L.GEMM_TN and glds and splitk == 1 and all(p.seg[j].K % 64 == 0 and p.seg[j].K > 0
                                                                 for p in chunk for j in range(p.nseg)):
-            return {41: "gemm_ntb_kernel<true, 6, %s, false>", 42: "gemm_ntb_kernel<false, 2, %s, false>",
-                    44: "gemm_ntb_kernel<true, 6, %s, true>"}[t] % str(layout == L.GEMM_NN).lower()
+            return {41: "gemm_ntb_kernel<true, 6, %s, false, 128>", 42: "gemm_ntb_kernel<false, 2, %s, false, 128>",
+                    44: "gemm_ntb_kernel<true, 6, %s, true, 128>",
+                    45: "gemm_ntb_kernel<true, 6, %s, true, 64>"}[t] % str(layout == L.GEMM_NN).lower()
         t = 20 if layout == L.GEMM_NT else 21
+    if t == 46:
+        if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
+            return "gemm_tnk_kernel<3, 1, true>"
+        t = 36
     if t in (38, 39, 40, 43):
         if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
             return {38: "gemm_tnb_kernel<false, 2, false>", 39: "gemm_tnb_kernel<true, 4, false>",
@@ -609,6 +620,7 @@ _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per
 
 
 _TNK_TILES_PER_PROBLEM = 48
+_TNR = os.environ.get("SCA_TNR", "1") != "0"  # A/B switch for variant 46
 
 
 # the 128x128 register-staged weight-gradient kernel with interleaved phases (tile 43) for long
@@ -904,6 +916,13 @@ def _weight_grads(items):
                 tile = 43
                 sk = _tnb_split(Kr, sum(-(-items[i][3].shape[0] // 128) * -(-items[i][3].shape[1] // 128)
                                         for i in sub))
+            elif _TNR and Kr % 64 == 0 and Kr >= 128:
+                # the k-split kernel with the register-staged, interleaved operand stream (variant
+                # 46): 6-20 % faster than both the LDS-DMA k-split (36) and the plain LDS-DMA
+                # kernel at every config-2 / 3 shape (tools/tn_library_compare.py,
+                # profiles/r05_tn/tnr_compare_*.log); split 2, or 4 when that makes exactly one
+                # full round of three workgroups per CU with >= 512 rows per split
+                tile, sk = 46, (4 if tiles * 4 == 768 and Kr >= 2048 else (2 if Kr >= 512 else 1))
             elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
                 # many-problem launches (an attention block's q/k/v/o of every stream) and big
                 # weights (an FFN's 768 x 256): the k-split outer-product kernel at split-K 2

@@ -118,10 +118,10 @@ def test_gemm_variant_ids_are_validated():
     from scattennet_amd import _lib
     lib = ctypes.CDLL(_lib.LIB_PATH)
     ERR, OK = 1, 0
-    for layout, bad in [(2, 41), (2, 45), (2, 30), (2, 23), (0, 36), (1, 37), (0, 38), (1, 40), (2, 44), (0, 43), (0, 11), (0, 2), (0, 99), (3, 0), (-1, 0)]:
+    for layout, bad in [(2, 41), (2, 45), (2, 30), (2, 23), (0, 36), (1, 37), (0, 38), (1, 40), (2, 44), (0, 43), (2, 45), (0, 46), (0, 11), (0, 2), (0, 99), (3, 0), (-1, 0)]:
         assert lib.sca_gemm_tile_override(layout, bad) == ERR, (layout, bad)
         assert lib.sca_gemm_variant(layout, 0, None, 1, None, None, bad, None) == ERR, (layout, bad)
-    for layout, good in [(0, 20), (1, 21), (2, 36), (2, 37), (2, 38), (2, 39), (2, 40), (2, 43), (0, 44), (1, 41), (2, 5), (1, 7), (0, 1), (2, 0)]:
+    for layout, good in [(0, 20), (1, 21), (2, 36), (2, 37), (2, 38), (2, 39), (2, 40), (2, 43), (0, 44), (1, 41), (0, 45), (1, 45), (2, 46), (2, 5), (1, 7), (0, 1), (2, 0)]:
         assert lib.sca_gemm_tile_override(layout, good) == OK, (layout, good)
         assert lib.sca_gemm_variant(layout, 0, None, 1, None, None, good, None) == OK, (layout, good)
     for layout in range(3):

@@ -14,8 +14,8 @@ def _prob(M, N, K, lda, ldb, A=0x1000, B=0x2000, nseg=1, alpha2=1.0):
 
 
 def test_tn_ksplit_tile_when_eligible():
-    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(256, 256, 2048, 256, 256)], 36) == "gemm_tnk_kernel<3, 1>"
-    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(256, 256, 2048, 256, 256)], 37) == "gemm_tnk_kernel<4, 1>"
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(256, 256, 2048, 256, 256)], 36) == "gemm_tnk_kernel<3, 1, false>"
+    assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(256, 256, 2048, 256, 256)], 37) == "gemm_tnk_kernel<4, 1, false>"
 
 
 def test_tn_ksplit_falls_back_like_the_launcher():
@@ -27,7 +27,17 @@ def test_tn_ksplit_falls_back_like_the_launcher():
     assert ops._gemm_kernel_name(L.GEMM_TN, [_prob(64, 64, 256, 64, 64, A=0x1004)], 36) == "gemm_kernel<2, T1, false>"
 
 
-def test_heuristic_names():
+def test_heuristic_names(monkeypatch):
+    # the register-staged 64x64 form by default (K % 64 == 0), 128x128 for 2048+ tiles and K >= 512
+    assert ops._gemm_kernel_name(L.GEMM_NT, [_prob(2048, 256, 256, 256, 256)], 0) == \
+        "gemm_ntb_kernel<true, 6, false, true, 64>"
+    assert ops._gemm_kernel_name(L.GEMM_NN, [_prob(2048, 256, 768, 768, 256)], 0) == \
+        "gemm_ntb_kernel<true, 6, true, true, 64>"
+    assert ops._gemm_kernel_name(L.GEMM_NT, [_prob(8192, 512, 512, 512, 512)] * 4, 0) == \
+        "gemm_ntb_kernel<true, 6, false, true, 128>"
+    # K % 64 != 0: the LDS-DMA kernels
+    assert ops._gemm_kernel_name(L.GEMM_NT, [_prob(2048, 256, 96, 96, 96)], 0) == "gemm_glds_kernel<0, 3>"
+    monkeypatch.setenv("SCA_NTB", "0")
     assert ops._gemm_kernel_name(L.GEMM_NT, [_prob(2048, 256, 256, 256, 256)], 0) == "gemm_glds_kernel<0, 3>"
     assert ops._gemm_kernel_name(L.GEMM_NN, [_prob(2048, 256, 768, 768, 256)], 0) == "gemm_glds_kernel<1, 2>"
     assert ops._gemm_kernel_name(L.GEMM_NN, [_prob(2046, 256, 768, 768, 256)], 0) == "gemm_kernel<1, T7>"

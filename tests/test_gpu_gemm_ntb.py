@@ -42,7 +42,7 @@ def _run(ops_, L, ops, tile, epi=0, gelu=False, drop=None, accum_base=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [41, 42, 44])
+@pytest.mark.parametrize("tile", [41, 42, 44, 45])
 def test_ntb_matches_float64(tile):
     from scattennet_amd import _lib as L, ops
     xs = _operands([(200, 132), (256, 384), (64, 4)], 192, seed=tile)
@@ -53,7 +53,7 @@ def test_ntb_matches_float64(tile):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [41, 42, 44])
+@pytest.mark.parametrize("tile", [41, 42, 44, 45])
 def test_ntb_gelu_accum_and_dropout_match_variant_20(tile):
     from scattennet_amd import _lib as L, ops
     xs = _operands([(300, 260), (128, 128)], 256, seed=7)
@@ -85,7 +85,7 @@ def test_ntb_hands_over_when_ineligible():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout_name", ["NT", "NN"])
-@pytest.mark.parametrize("tile", [41, 42, 44])
+@pytest.mark.parametrize("tile", [41, 42, 44, 45])
 def test_ntb_segments_nt_and_nn(layout_name, tile):
     """Three segments (the dX = dQ Wq + dK Wk + dV Wv form) of different K, NT and NN (B [K][N],
     transposed into the LDS image), M / N not multiples of 128, against float64 and against the

@@ -53,7 +53,7 @@ def _check(items, alpha=1.0, bscale=1.0, base=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 37, 38, 39, 40, 43])
+@pytest.mark.parametrize("tile", [36, 37, 38, 39, 40, 43, 46])
 @pytest.mark.parametrize("splitk,fused", [(1, False), (2, False), (2, True), (3, True), (5, True)])
 def test_ksplit_kernel_matches_float64(tile, splitk, fused):
     """gemm_tnk_kernel (tiles 36 / 37) and gemm_tnb_kernel (38): M not a multiple of 64 / 128,
@@ -99,13 +99,13 @@ def test_tnb_tile_falls_back_when_k_is_not_a_multiple_of_64():
     from scattennet_amd import ops
     items = _case([(128, 128), (100, 36)], 992, seed=6)
     probs = _probs(items)
-    assert ops._gemm_kernel_name(2, probs, 38) == "gemm_tnk_kernel<3, 1>"
+    assert ops._gemm_kernel_name(2, probs, 38) == "gemm_tnk_kernel<3, 1, false>"
     _ksplit(items, tile=38, splitk=2)
     _check(items)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 38, 39, 43])
+@pytest.mark.parametrize("tile", [36, 38, 39, 43, 46])
 def test_ksplit_bias_off_and_accumulate(tile):
     items = _case([(128, 192)] * 3, 512, seed=5, bias=False)
     base = [torch.randn(128, 192, device="cuda") for _ in items]
@@ -116,7 +116,7 @@ def test_ksplit_bias_off_and_accumulate(tile):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [36, 38, 39, 43])
+@pytest.mark.parametrize("tile", [36, 38, 39, 43, 46])
 def test_ksplit_is_deterministic(tile):
     """The split-K slabs are summed in slice order whichever split arrives last."""
     items = _case([(256, 256)] * 6, 2048, seed=9)

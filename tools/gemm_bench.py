@@ -13,7 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4", 41: "NTB128i", 42: "NTB128", 44: "NTB128il"}
+TILES = {1: "64x64", 5: "64s1", 7: "128x64w8", 20: "G64s3", 21: "G64s2", 22: "G64s4", 41: "NTB128i", 42: "NTB128", 44: "NTB128il", 45: "NTB64il"}
 
 
 def make_case(name, layout, shapes, splitk=1, segs=1):

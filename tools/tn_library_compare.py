@@ -18,6 +18,7 @@ from scattennet_amd import _lib as L, ops  # noqa: E402
 PEAK = 157.3
 SPLITS = (1, 2, 3, 4, 5, 6, 8)  # --splits
 TNB_TILES = (38, 39, 40, 43)  # --tnb-tiles
+KSPLIT_TILES = (36, 46)  # --ksplit-tiles
 LIBRARY = False  # --library: the hipBLASLt timings only, eagerly, in a process that captures no graph
 
 
@@ -38,16 +39,19 @@ def variants(c):
     P = probs(c)
     out = []
     tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
-    for sk in (2, 3):
+    for sk in (2, 3, 4):
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
-        out.append((f"ksplit36 sk={sk} wg={tiles * sk}", lambda sk=sk, ws=ws: ops.gemm(L.GEMM_TN, P, splitk=sk, ws=ws,
-                                                                                       tile=36)))
+        for tl in KSPLIT_TILES:
+            out.append((f"ksplit{tl} sk={sk} wg={tiles * sk}", lambda sk=sk, ws=ws, tl=tl: ops.gemm(
+                L.GEMM_TN, P, splitk=sk, ws=ws, tile=tl)))
     t128 = sum(-(-dW.shape[0] // 128) * -(-dW.shape[1] // 128) for _, _, dW, _ in c["items"])
     for sk in SPLITS:
         if c["K"] // sk < 256 and sk > 1:
             continue
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
         for tl in TNB_TILES:
+            if not tl:
+                continue
             out.append((f"tnb{tl} sk={sk} wg={t128 * sk}", lambda sk=sk, ws=ws, tl=tl: ops.gemm(
                 L.GEMM_TN, P, splitk=sk, ws=ws, tile=tl)))
     if LIBRARY and len({dW.shape for _, _, dW, _ in c["items"]}) == 1:
@@ -73,9 +77,11 @@ def main():
                                                    "(tools/tn_pmc2.py)")
     ap.add_argument("--splits", default="1,2,3,4,5,6,8", help="split-K values of the 128x128 kernels")
     ap.add_argument("--tnb-tiles", default="38,39,40,43", help="variant ids of the 128x128 kernel")
+    ap.add_argument("--ksplit-tiles", default="36,46", help="variant ids of the 64x64 k-split kernel")
     args = ap.parse_args()
-    global LIBRARY, SPLITS, TNB_TILES
-    SPLITS = tuple(int(x) for x in args.splits.split(","))
+    global LIBRARY, SPLITS, TNB_TILES, KSPLIT_TILES
+    KSPLIT_TILES = tuple(int(x) for x in args.ksplit_tiles.split(",") if x)
+    SPLITS = tuple(int(x) for x in args.splits.split(",") if int(x) > 0)
     TNB_TILES = tuple(int(x) for x in args.tnb_tiles.split(","))
     LIBRARY = args.library
     torch.manual_seed(0)
