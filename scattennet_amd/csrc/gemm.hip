@@ -1469,6 +1469,133 @@ __global__ __launch_bounds__(256, 1) void gemm_ntb_kernel(const GemmArgs args) {
   }
 }
 
+// ------------------------------------------------------------------------------ row-tile main loop
+// The main loop of the LayerNorm-fused GEMMs (32 full rows x 256 columns, 512 threads, wave w
+// owning columns 32w .. 32w+31 as 2 x 2 16x16 blocks) in the register-staged, interleaved form
+// of gemm_ntb_kernel: per 64-k iteration one A piece and eight B pieces per thread, the
+// A [32][68] and B [256][68] (k-contiguous, NN's B transposed on the store) images read whole
+// into registers, loads / stores issued between the MFMAs.  Segments back to back; every
+// segment's K % 64 == 0.  acc[i][j]: rows 16i + 4(lane >> 4) + r, columns 32w + 16j + (lane & 15).
+constexpr int LR_SMEM = (32 + 256) * 68 * 4;  // 78 KB
+template <bool B_KN>
+__device__ __forceinline__ void ln_rows_reg(const sca_gemm_problem& P, int m0, float* lds, f32x4 (&acc)[2][2]) {
+  constexpr int LD = 68, NPRE = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kg = lane >> 4, li = lane & 15;
+  float* Ai = lds;
+  float* Bi = lds + 32 * LD;
+  const int nseg = P.nseg;
+  const int it0 = P.seg[0].K / 64, it1 = nseg > 1 ? P.seg[1].K / 64 : 0;
+  const int nit = it0 + it1 + (nseg > 2 ? P.seg[2].K / 64 : 0);
+  const int arow = tid >> 4, ak4 = 4 * (tid & 15);
+  f32x4 st[9];
+  auto load = [&](int it) {
+    int sg = 0, lit = it;
+    if (lit >= it0) {
+      lit -= it0;
+      sg = 1;
+      if (lit >= it1) {
+        lit -= it1;
+        sg = 2;
+      }
+    }
+    const sca_gemm_seg& G = P.seg[sg];
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(G.A), 0, (int)(((long)(P.M - 1) * G.lda + G.K) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(G.B), 0,
+        (int)((B_KN ? (long)(G.K - 1) * G.ldb + P.N : (long)(P.N - 1) * G.ldb + G.K) * 4), 0x00020000);
+    st[0] = tb_load(ra, (int)(((long)min(m0 + arow, P.M - 1) * G.lda + ak4) * 4), lit * 256);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (B_KN) {
+        const int b = 8 * wave + j, k = 16 * (b & 3) + li, c4 = 4 * (4 * (b >> 2) + kg);
+        st[1 + j] = tb_load(rb, (k * G.ldb + c4) * 4, lit * 64 * G.ldb * 4);
+      } else {
+        st[1 + j] = tb_load(rb, ((arow + 32 * j) * G.ldb + ak4) * 4, lit * 256);
+      }
+    }
+  };
+  auto store = [&]() {
+    st4(Ai + arow * LD + ak4, st[0]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (B_KN) {
+        const int b = 8 * wave + j, k = 16 * (b & 3) + li, c4 = 4 * (4 * (b >> 2) + kg);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bi[(c4 + q) * LD + k] = st[1 + j][q];
+      } else {
+        st4(Bi + (arow + 32 * j) * LD + ak4, st[1 + j]);
+      }
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* ra_lds = Ai + li * LD + 4 * kg;
+  const float* rb_lds = Bi + (32 * wave + li) * LD + 4 * kg;
+  auto iter = [&](auto wr_c, auto ld_c, int it) {
+    constexpr bool WR = decltype(wr_c)::value, LDN = decltype(ld_c)::value;
+    f32x4 a[4][2], b[4][2];
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        a[kc][q] = ld4(ra_lds + 16 * q * LD + 16 * kc);
+        b[kc][q] = ld4(rb_lds + 16 * q * LD + 16 * kc);
+      }
+    auto steps = [&](int t0, int t1) {
+#pragma unroll
+      for (int t = t0; t < t1; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a[t >> 2][i][t & 3], b[t >> 2][j][t & 3], acc[i][j]);
+    };
+    steps(0, NPRE);
+    ilv_read<0, 4, 4, NPRE>();
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WR) {
+      store();
+      if constexpr (LDN) load(it + 2);
+    }
+    steps(NPRE, 16);
+    if constexpr (WR) ilv_store<0, 9, B_KN ? 4 : 1, 5>();
+    __syncthreads();
+  };
+  if (nit > 0) {
+    load(0);
+    store();
+    if (nit > 1) load(1);
+    __syncthreads();
+  }
+  int it = 0;
+#pragma unroll 1
+  for (; it + 2 < nit; ++it) iter(std::true_type{}, std::true_type{}, it);
+  if (it + 1 < nit) iter(std::true_type{}, std::false_type{}, it++);
+  if (it < nit) iter(std::false_type{}, std::false_type{}, it);
+}
+
+// the row-tile main loop's requirements: every segment's K % 64 == 0, 32-bit operand offsets
+bool ln_reg_ok(const sca_gemm_problem& P, bool b_kn) {
+  const long lim = (1L << 31) - 1;
+  for (int s = 0; s < P.nseg; ++s) {
+    const sca_gemm_seg& G = P.seg[s];
+    if (G.K % 64 || G.K == 0) return false;
+    if (((long)P.M * G.lda + G.K) * 4 > lim) return false;
+    if ((b_kn ? (long)G.K * G.ldb + P.N : (long)P.N * G.ldb + G.K) * 4 > lim) return false;
+  }
+  return true;
+}
+
+// SCA_LNREG=0 keeps the LayerNorm-fused GEMMs on their LDS-DMA main loops (A/B), read once
+bool ln_reg_default() {
+  static const bool on = !(getenv("SCA_LNREG") && atoi(getenv("SCA_LNREG")) == 0);
+  return on;
+}
+
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
 // v = resid + dropout((A B^T + bias) * post_scale), y = LayerNorm(v) * gamma + beta, for
@@ -1548,7 +1675,7 @@ __device__ __forceinline__ void chain_rows(const sca_gemm_chain_pass& Q, const f
 // NC = 2: d_model = 512 as two 256-column halves of one continuous slice sequence (the A
 // tile is re-read from L2 once; two accumulators per wave), one 32 x 512 epilogue tile and
 // LayerNorm over the full row; no chained passes.
-template <int BM, bool CH, int NC>
+template <int BM, bool CH, int NC, bool REG = false>
 __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmLnArgs args) {
   using CF = LgCfg<BM>;
   constexpr int S = CF::S;
@@ -1556,6 +1683,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   constexpr int NROW = NC * LG_BN;
   static_assert(!CH || (BM == 32 && LG_CH_SMEM >= S * CF::STAGE && 32 * LG_VS * 4 <= LG_A2_OFF), "LDS map");
   static_assert(NC == 1 || (NC == 2 && BM == 32 && !CH && 32 * VS * 4 <= S * CF::STAGE), "LDS map (NC = 2)");
+  static_assert(!REG || (BM == 32 && NC == 1 && LR_SMEM <= S * CF::STAGE), "LDS map (REG)");
   __shared__ __attribute__((aligned(1024))) char smem[CH ? LG_CH_SMEM : S * CF::STAGE];
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
@@ -1627,7 +1755,18 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   }
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = G.alpha;
-  if constexpr (BM == 32) {
+  if constexpr (REG) {
+    f32x4 acc[2][2];
+    ln_rows_reg<false>(P, m0, V, acc);
+    SCA_LN_STAMP(1);
+    const int li = lane & 15, kg = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) V[(16 * i + 4 * kg + r) * VS + 32 * wave + 16 * j + li] = acc[i][j][r] * alpha;
+  } else if constexpr (BM == 32) {
     f32x16 acc[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -1896,7 +2035,7 @@ struct GemmLnbArgs {
 
 // NC = 2: d_model = 512 as two 256-column halves (one continuous slice sequence, two
 // accumulators per wave), a 32 x 512 epilogue tile, no chained GEMM.
-template <int NC>
+template <int NC, bool REG = false>
 __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   if constexpr (SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
   __shared__ __attribute__((aligned(1024))) char smem[LB_SMEM];
@@ -1904,6 +2043,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   constexpr int RED_OFF = NC == 1 ? LB_RED_OFF : LB_BM * VS * 4;  // dgamma / dbeta wave partials
   static_assert(LB_B2 >= LB_BM * LG_VS * 4 && LB_RED_OFF + 2 * 8 * LG_BN * 4 <= LB_SMEM, "LDS map");
   static_assert(NC == 1 || RED_OFF + 2 * 8 * NROW * 4 <= LB_SMEM, "LDS map (NC = 2)");
+  static_assert(!REG || (NC == 1 && LR_SMEM <= LB_SMEM), "LDS map (REG)");
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
   const unsigned orig = blockIdx.x + gx * blockIdx.z;
@@ -1982,6 +2122,10 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
   const int col = lane & 31, h = lane >> 5;
+  f32x4 racc[2][2];
+  if constexpr (REG) {
+    ln_rows_reg<true>(P, m0, reinterpret_cast<float*>(smem), racc);
+  } else {
 #pragma unroll
   for (int i = 0; i < LB_S - 1; ++i)
     if (i < ttot) dma(i, i);
@@ -2012,16 +2156,27 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   for (int t = 0; t < total; ++t) slice(t, acc[0]);
   if constexpr (NC == 2)
     for (int t = total; t < ttot; ++t) slice(t, acc[1]);
+  }
   // 32 x 256 NC tile -> LDS (the ring is free once every wave has passed its last slice)
   __syncthreads();
   float* V = reinterpret_cast<float*>(smem);
   const float alpha = P.seg[0].alpha;
   const int rowh = 4 * h;
+  if constexpr (REG) {
+    const int li = lane & 15, kg = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) V[(16 * i + 4 * kg + r) * VS + 32 * wave + 16 * j + li] = racc[i][j][r] * alpha;
+  } else {
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       V[((r & 3) + 8 * (r >> 2) + rowh) * VS + LG_BN * c + 32 * wave + col] = acc[c][r] * alpha;
+  }
   __syncthreads();
 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue operands have landed (see gemm_ln_kernel)
@@ -2692,11 +2847,21 @@ extern "C" int sca_gemm_ln(int nprob, const sca_gemm_problem* probs, const sca_g
   if (N != LG_BN) {
     hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 2>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   } else if (chain) {
-    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true, 1>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+    bool reg = ln_reg_default();
+    for (int i = 0; i < nprob; ++i) reg = reg && ln_reg_ok(probs[i], false);
+    if (reg)
+      hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true, 1, true>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, true, 1>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   } else if (bm == 16) {
     hipLaunchKernelGGL((gemm_ln_kernel<GL_A16, false, 1>), dim3((maxM + 15) / 16, 1, nprob), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 1>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+    bool reg = ln_reg_default();
+    for (int i = 0; i < nprob; ++i) reg = reg && ln_reg_ok(probs[i], false);
+    if (reg)
+      hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 1, true>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm_ln_kernel<GL_A32, false, 1>), dim3((maxM + 31) / 32, 1, nprob), dim3(512), 0, st, a);
   }
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_ln: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
@@ -2752,7 +2917,10 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
   }
   if (maxM == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (N == LG_BN) hipLaunchKernelGGL(gemm_lnb_kernel<1>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  bool reg = N == LG_BN && ln_reg_default();
+  for (int i = 0; i < nprob; ++i) reg = reg && ln_reg_ok(probs[i], true);
+  if (reg) hipLaunchKernelGGL((gemm_lnb_kernel<1, true>), dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  else if (N == LG_BN) hipLaunchKernelGGL(gemm_lnb_kernel<1>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   else hipLaunchKernelGGL(gemm_lnb_kernel<2>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
