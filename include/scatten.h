@@ -219,9 +219,13 @@ int sca_gemm_lnb_blocks(int M);
 
 /* Tuning knob: force the kernel variant of one layout for every later sca_gemm* call
  * (0 = built-in heuristic; 1 / 5 / 7 register-staged 64x64 / single-buffered 64x64 /
- * 128x64 8 waves; 20 / 21 / 22 LDS-DMA 64x64 with a 3- / 2- / 4-stage ring; 36 / 37, TN
- * only: the k-split weight-gradient kernel with a 3- / 4-stage ring — every variant computes
- * the full result).  Any other id: SCA_ERR_ARG, nothing changed.  Process-global.          */
+ * 128x64 8 waves; 20 / 21 / 22 LDS-DMA 64x64 with a 3- / 2- / 4-stage ring; TN only: 36 / 37
+ * the k-split weight-gradient kernel with a 3- / 4-stage ring, 46 the same with the
+ * register-staged interleaved operand stream, 38 / 39 / 40 / 43 128x128 register-staged
+ * (43: interleaved phases); NT / NN only: 41 / 42 / 44 128x128 and 45 64x64 register-staged
+ * (44, 45: interleaved) — every variant computes the full result; a shape a variant cannot
+ * take runs on the LDS-DMA kernels).  Any other id: SCA_ERR_ARG, nothing changed.
+ * Process-global.                                                                          */
 int sca_gemm_tile_override(int layout, int tile);
 /* sca_gemm with the kernel variant chosen for this call only (ids as above, 0 = the override
  * or heuristic; an invalid id is SCA_ERR_ARG): split-K slabs combined in-launch when

@@ -1631,6 +1631,11 @@ constexpr int LG_A2_LD = 260;
 constexpr int LG_A2_OFF = 2 * LG_B_BYTES;
 constexpr int LG_SCR_OFF = LG_A2_OFF + 32 * LG_A2_LD * 4;
 constexpr int LG_CH_SMEM = LG_SCR_OFF + 8 * 32 * EPI_LD * 4;
+// register-staged chained passes (REG): the pass's B image [256][68] first, then the y tile,
+// then the scratches (140.5 KB)
+constexpr int LR_A2_OFF = 256 * 68 * 4;
+constexpr int LR_SCR_OFF = LR_A2_OFF + 32 * LG_A2_LD * 4;
+constexpr int LR_CH_SMEM = LR_SCR_OFF + 8 * 32 * EPI_LD * 4;
 
 struct GemmLnArgs {
   sca_gemm_problem p[SCA_GEMM_LN_MAX_PROBLEMS];
@@ -1684,7 +1689,9 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   static_assert(!CH || (BM == 32 && LG_CH_SMEM >= S * CF::STAGE && 32 * LG_VS * 4 <= LG_A2_OFF), "LDS map");
   static_assert(NC == 1 || (NC == 2 && BM == 32 && !CH && 32 * VS * 4 <= S * CF::STAGE), "LDS map (NC = 2)");
   static_assert(!REG || (BM == 32 && NC == 1 && LR_SMEM <= S * CF::STAGE), "LDS map (REG)");
-  __shared__ __attribute__((aligned(1024))) char smem[CH ? LG_CH_SMEM : S * CF::STAGE];
+  static_assert(!(REG && CH) || (32 * LG_VS * 4 <= LR_A2_OFF && LR_CH_SMEM <= 160 * 1024), "LDS map (REG, chained)");
+  constexpr int A2OFF = REG ? LR_A2_OFF : LG_A2_OFF, SCROFF = REG ? LR_SCR_OFF : LG_SCR_OFF;
+  __shared__ __attribute__((aligned(1024))) char smem[CH ? (REG ? LR_CH_SMEM : LG_CH_SMEM) : S * CF::STAGE];
   const unsigned gx = gridDim.x;
   const unsigned nwg = gx * gridDim.z;
   const unsigned orig = blockIdx.x + gx * blockIdx.z;
@@ -1871,10 +1878,34 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       s[i] += (x[0] + x[1]) + (x[2] + x[3]);
     }
   }
+  // REG chained passes: iteration u = 64 k rows of pass pass_of(u >> 2); thread's pieces j < 8:
+  // B rows (tid >> 4) + 32j, k 4 (tid & 15) .. +3 — the first one loaded under the LayerNorm
+  const int nit2 = CH && REG ? 4 * LN.npass : 0;
+  f32x4 st2[8];
+  auto load2 = [&](int u) {
+    int q = (u >> 2) + (args.rot && LN.npass > 0 ? bx % LN.npass : 0);
+    q = q >= LN.npass ? q - LN.npass : q;
+    const sca_gemm_chain_pass& Q = LN.pass[q];
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(Q.B), 0, (int)(((long)(LG_BN - 1) * Q.ldb + LG_BN) * 4), 0x00020000);
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      st2[j] = tb_load(rb, (((t >> 4) + 32 * j) * Q.ldb + 4 * (t & 15)) * 4, (u & 3) * 256);
+  };
+  auto store2 = [&]() {
+    float* Bi = reinterpret_cast<float*>(smem);
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st4(Bi + ((t >> 4) + 32 * j) * 68 + 4 * (t & 15), st2[j]);
+  };
+  if constexpr (CH && REG) {
+    if (nit2 > 0) load2(0);
+  }
   // chained passes: a slice of B (row r of the [256][32] image at r * 128 B, pieces 4w .. 4w+3
   // by wave w) — the first two stream in under the LayerNorm math, into the V tile's region
   // once every wave has read its rows of it
-  const int nsl = CH ? 8 * LN.npass : 0;
+  const int nsl = CH && !REG ? 8 * LN.npass : 0;
   // every workgroup streams the same weights in near lock-step; row tile bx runs the passes
   // from pass bx % npass on, so that neighbouring tiles stream different weight matrices at
   // a time (each pass's own K order is unchanged: bit-identical results; +0.5 % in step,
@@ -1894,8 +1925,13 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
   };
   if constexpr (CH) {
     __syncthreads();
-    if (nsl > 0) dma2(0, 0);
-    if (nsl > 1) dma2(1, 1);
+    if constexpr (REG) {
+      if (nit2 > 0) store2();
+      if (nit2 > 1) load2(1);
+    } else {
+      if (nsl > 0) dma2(0, 0);
+      if (nsl > 1) dma2(1, 1);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
@@ -1923,7 +1959,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const f32x4 y = (v[i][c] - mean) * rstd * gam[c] + bet[c];
-      if (CH) st4(reinterpret_cast<float*>(smem + LG_A2_OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
+      if (CH) st4(reinterpret_cast<float*>(smem + A2OFF) + lr * LG_A2_LD + n, y);  // rows past M: finite
       if (m < P.M) {
         st4g(P.C + (long)m * P.ldc + LG_BN * c + n, v[i][c]);
         st4g(LN.y + (long)m * NROW + LG_BN * c + n, y);
@@ -1936,7 +1972,83 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       }
     }
   }
-  if constexpr (CH) {
+  if constexpr (CH && REG) {
+    // chained NT GEMMs, register-staged: out_p[32 x 256] = y_tile B_p^T, A fragments from the
+    // y image, B through the [256][68] image (ln_rows_reg's arrangement), 4 iterations a pass
+    const float* A2 = reinterpret_cast<const float*>(smem + A2OFF);
+    const float* Bi = reinterpret_cast<const float*>(smem);
+    float* scratch = reinterpret_cast<float*>(smem + SCROFF) + wave * 32 * EPI_LD;
+    const int li = lane & 15, kg = lane >> 4;
+    const int prot2 = args.rot && LN.npass > 0 ? bx % LN.npass : 0;
+    f32x4 acc2[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    lds_barrier();  // the y rows and pass 0's first B tile are in LDS
+    SCA_LN_STAMP(2);
+    auto iter2 = [&](auto wr_c, auto ld_c, int u) {
+      constexpr bool WR = decltype(wr_c)::value, LDN = decltype(ld_c)::value;
+      f32x4 a[4][2], b[4][2];
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          a[kc][q] = ld4(A2 + (16 * q + li) * LG_A2_LD + 64 * (u & 3) + 16 * kc + 4 * kg);
+          b[kc][q] = ld4(Bi + (32 * wave + 16 * q + li) * 68 + 16 * kc + 4 * kg);
+        }
+      auto steps = [&](int t0, int t1) {
+#pragma unroll
+        for (int t = t0; t < t1; ++t)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc2[i][j] = mfma16(a[t >> 2][i][t & 3], b[t >> 2][j][t & 3], acc2[i][j]);
+      };
+      steps(0, 4);
+      ilv_read<0, 4, 4, 4>();
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();  // every wave has read the B image
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (WR) {
+        store2();
+        if constexpr (LDN) load2(u + 2);
+      }
+      steps(4, 16);
+      if constexpr (WR) ilv_store<0, 8, 1, 6>();
+      if ((u & 3) == 3) {  // the pass's 32 x 256 block: this wave's 32 x 32 through its scratch
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) scratch[(16 * i + 4 * kg + r) * EPI_LD + 16 * j + li] = acc2[i][j][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        f32x4 rows[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rows[q] = ld4(scratch + ((lane >> 3) + 8 * q) * EPI_LD + 4 * (lane & 7));
+        int pq = (u >> 2) + prot2;
+        pq = pq >= LN.npass ? pq - LN.npass : pq;
+        chain_rows(LN.pass[pq], rows, m0, P.M, 32 * wave, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // scratch reads done before the next pass
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      __syncthreads();  // the next B tile is in LDS
+    };
+    int u = 0;
+#pragma unroll 1
+    for (; u + 2 < nit2; ++u) iter2(std::true_type{}, std::true_type{}, u);
+    if (u + 1 < nit2) iter2(std::true_type{}, std::false_type{}, u++);
+    if (u < nit2) iter2(std::false_type{}, std::false_type{}, u);
+  }
+  if constexpr (CH && !REG) {
     // chained NT GEMMs: out_p[32 x 256] = y_tile[32 x 256] B_p^T — A from the LDS image
     // (published by the barrier below), B through the 2-stage ring one slice ahead;
     // the passes are one continuous slice sequence (the next pass's first slice streams in

@@ -380,7 +380,7 @@ def _attach_ln_saved(ys, vs, means, rstds, gam, wo=None, aux=None):
     return objs
 
 
-_CHAIN_NEXT = True
+_CHAIN_NEXT = os.environ.get("SCA_CHAIN", "1") != "0"  # A/B switch
 
 
 class NextProjections:
@@ -621,6 +621,7 @@ _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per
 
 _TNK_TILES_PER_PROBLEM = 48
 _TNR = os.environ.get("SCA_TNR", "1") != "0"  # A/B switch for variant 46
+_TNR_SK = int(os.environ.get("SCA_TNR_SK", "0"))  # A/B: one split-K for every variant-46 launch
 
 
 # the 128x128 register-staged weight-gradient kernel with interleaved phases (tile 43) for long
@@ -733,14 +734,18 @@ _WGRAD_SIDE = True
 _EARLY_FORK = True   # fork the weight gradients before the layer's input-gradient launch
 _side_streams = {}
 _join_pending = {}
+# weight-gradient side streams per device, used round-robin by successive weight_grads calls
+# (SCA_WGRAD_STREAMS, A/B: with 2 the tail of consecutive dW launches can overlap)
+_WGRAD_STREAMS = max(1, int(os.environ.get("SCA_WGRAD_STREAMS", "1")))
 
 
 def _side_stream(device):
-    st = _side_streams.get(device)
-    if st is None:
-        st = torch.cuda.Stream(device=device)
-        _side_streams[device] = st
-    return st
+    ent = _side_streams.get(device)
+    if ent is None:
+        ent = _side_streams[device] = [[torch.cuda.Stream(device=device) for _ in range(_WGRAD_STREAMS)], 0]
+    streams, i = ent
+    ent[1] = (i + 1) % len(streams)
+    return streams[i]
 
 
 class ForkLedger:
@@ -923,6 +928,8 @@ def _weight_grads(items):
                 # profiles/r05_tn/tnr_compare_*.log); split 2, or 4 when that makes exactly one
                 # full round of three workgroups per CU with >= 512 rows per split
                 tile, sk = 46, (4 if tiles * 4 == 768 and Kr >= 2048 else (2 if Kr >= 512 else 1))
+                if _TNR_SK and Kr // _TNR_SK >= 256:
+                    sk = _TNR_SK
             elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
                 # many-problem launches (an attention block's q/k/v/o of every stream) and big
                 # weights (an FFN's 768 x 256): the k-split outer-product kernel at split-K 2
