@@ -322,11 +322,20 @@ def gemm_ln(probs, lns, eps):
         chain = any(ln.npass > 0 for ln in lchunk)
         nc = chunk[0].N // 256
         bm = 32 if nc > 1 else lib.sca_gemm_ln_rows(len(chunk), max(p.M for p in chunk), int(chain))
-        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}>", flops):
+        reg = nc == 1 and bm == 32 and _ln_reg(chunk)
+        with _timed(f"gemm_ln_kernel<{bm}, {'true' if chain else 'false'}, {nc}, {'true' if reg else 'false'}>",
+                    flops):
             L.check(lib.sca_gemm_ln(len(chunk), arr, larr, float(eps), st), "sca_gemm_ln")
 
 
 _FUSE_LNB = True
+
+
+def _ln_reg(probs):
+    """Whether sca_gemm_ln / sca_gemm_lnb run the register-staged main loop (gemm.hip ln_reg_ok:
+    every segment's K % 64 == 0; SCA_LNREG=0 switches it off) — for the kernel names."""
+    return os.environ.get("SCA_LNREG", "1") != "0" and \
+        all(p.seg[j].K % 64 == 0 and p.seg[j].K > 0 for p in probs for j in range(p.nseg))
 
 
 class LnSaved:
@@ -493,7 +502,8 @@ def gemm_lnb(probs, lnp):
     flops = sum(2.0 * p.M * p.N * p.seg[j].K for p in probs for j in range(p.nseg)) if _PROFILER else 0.0
     if chain and _PROFILER:
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
-    with _timed(f"gemm_lnb_kernel<{probs[0].N // 256}>", flops):
+    nc = probs[0].N // 256
+    with _timed(f"gemm_lnb_kernel<{nc}, {'true' if nc == 1 and _ln_reg(probs) else 'false'}>", flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
 
