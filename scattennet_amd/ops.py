@@ -279,7 +279,7 @@ def gemm(layout, probs, splitk=1, ws=None, tile=0):
 
 
 # the fused LayerNorms' dgamma / dbeta reductions ride in the weight-gradient side section
-_LN_AFFINE_SIDE = True
+_LN_AFFINE_SIDE = os.environ.get("SCA_LN_AFFINE_SIDE", "1") != "0"  # A/B switch
 
 # GEMM + post-LN LayerNorm in one launch (sca_gemm_ln) where the shape allows it
 _FUSE_LN = True
@@ -290,7 +290,7 @@ _FUSE_LN = True
 # the 32-row x 256-column tiles at one workgroup per CU run the big-M GEMMs at ~0.43 of
 # peak against the plain kernel's ~0.6, which outweighs the LayerNorm launches saved;
 # DESIGN.md §9) — opt-in (tests switch it on)
-_FUSE_LN512 = False
+_FUSE_LN512 = os.environ.get("SCA_FUSE_LN512", "0") == "1"  # opt-in (A/B)
 
 
 def ln_width_ok(N):
