@@ -2898,8 +2898,9 @@ extern "C" int sca_gemm_ln_rows(int nprob, int maxM, int chain) {
   if (chain) return 32;
   if (bm_force) return bm_force;
   // the register-staged 32-row loop beats the 16-row LDS-DMA tiles even below one workgroup
-  // per CU (config 3: 1605 -> 1630 clips/s, profiles/r05_ntb/ln_rows_cfg3_ab.txt)
-  if (ln_reg_default()) return 32;
+  // per CU (config 3: 1605 -> 1630 clips/s, profiles/r05_ntb/ln_rows_cfg3_ab.txt), but not
+  // at a quarter of the CUs (1 x (2048, 256, 256): 13.7 vs 10.7 us, tools/gemm_ln_bench.py)
+  if (ln_reg_default() && wg32 >= 128) return 32;
   return wg32 >= 256 ? 32 : 16;
 }
 
