@@ -19,6 +19,7 @@ PEAK = 157.3
 SPLITS = (1, 2, 3, 4, 5, 6, 8)  # --splits
 TNB_TILES = (38, 39, 40, 43)  # --tnb-tiles
 KSPLIT_TILES = (36, 46)  # --ksplit-tiles
+KSPLIT_SPLITS = (2, 3, 4)  # --ksplit-splits
 LIBRARY = False  # --library: the hipBLASLt timings only, eagerly, in a process that captures no graph
 
 
@@ -39,7 +40,7 @@ def variants(c):
     P = probs(c)
     out = []
     tiles = sum(-(-dW.shape[0] // 64) * -(-dW.shape[1] // 64) for _, _, dW, _ in c["items"])
-    for sk in (2, 3, 4):
+    for sk in KSPLIT_SPLITS:
         ws = torch.empty(sum(sk * (dW.numel() + dW.shape[0]) for _, _, dW, _ in c["items"]), device="cuda")
         for tl in KSPLIT_TILES:
             out.append((f"ksplit{tl} sk={sk} wg={tiles * sk}", lambda sk=sk, ws=ws, tl=tl: ops.gemm(
@@ -78,9 +79,11 @@ def main():
     ap.add_argument("--splits", default="1,2,3,4,5,6,8", help="split-K values of the 128x128 kernels")
     ap.add_argument("--tnb-tiles", default="38,39,40,43", help="variant ids of the 128x128 kernel")
     ap.add_argument("--ksplit-tiles", default="36,46", help="variant ids of the 64x64 k-split kernel")
+    ap.add_argument("--ksplit-splits", default="2,3,4", help="split-K values of the 64x64 k-split kernels")
     args = ap.parse_args()
-    global LIBRARY, SPLITS, TNB_TILES, KSPLIT_TILES
+    global LIBRARY, SPLITS, TNB_TILES, KSPLIT_TILES, KSPLIT_SPLITS
     KSPLIT_TILES = tuple(int(x) for x in args.ksplit_tiles.split(",") if x)
+    KSPLIT_SPLITS = tuple(int(x) for x in args.ksplit_splits.split(",") if x)
     SPLITS = tuple(int(x) for x in args.splits.split(",") if int(x) > 0)
     TNB_TILES = tuple(int(x) for x in args.tnb_tiles.split(","))
     LIBRARY = args.library
