@@ -433,7 +433,7 @@ typedef struct {
   float scale;
 } sca_reduce_problem;
 
-#define SCA_REDUCE_MAX_PROBLEMS 16
+#define SCA_REDUCE_MAX_PROBLEMS 64
 int sca_reduce_rows(int nprob, const sca_reduce_problem* probs, int S, int I, int N, long stride_s,
                     long stride_i, int accumulate, void* stream);
 

@@ -21,7 +21,7 @@ GEMM_LN_MAX_PROBLEMS = 8
 GEMM_MAX_PROBLEMS = 16
 ATTN_MAX_PROBLEMS = 8
 LN_MAX_PROBLEMS = 8
-REDUCE_MAX_PROBLEMS = 16
+REDUCE_MAX_PROBLEMS = 64
 MAP_MAX_PROBLEMS = 8
 POOL_MAX_PROBLEMS = 8
 SOFTMAX_MAX_PROBLEMS = 8

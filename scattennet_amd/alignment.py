@@ -23,6 +23,7 @@ from torch.autograd import Function
 from . import _lib as L
 from . import ops
 from .ops import _prob, _seg, gemm
+from .precision import fp32_compute
 
 # split-K of the per-step recurrent GEMMs (M = B rows only): forward K = H, backward K = 4H
 # would otherwise run on N/64 workgroups per direction
@@ -151,6 +152,7 @@ class AlignmentModule(nn.Module):
                            dropout=dropout, bidirectional=bidirectional)
         self.gloss_layer = nn.Linear(hidden_size, cls_num)
 
+    @fp32_compute()
     def forward(self, x):
         # the caller's (T, B, C) is the permute(1, 0, 2) view of a batch-major tensor
         # (model/__init__.py:52): permuting back is free

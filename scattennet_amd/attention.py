@@ -13,6 +13,7 @@ import torch
 from torch import nn
 
 from . import library, ops
+from .precision import fp32_compute
 
 
 class BaseAttention(nn.Module):
@@ -144,6 +145,7 @@ class SelfAttention(BaseAttention):
             raise ValueError("d_model must be divisible by num_heads")
         self._reinit_projections(d_model, bias)
 
+    @fp32_compute()
     def forward(self, hidden_states, attention_mask):
         return attention_grouped([self], "self", [hidden_states], None, attention_mask)[0]
 
@@ -158,6 +160,7 @@ class CrossAttention(BaseAttention):
             raise ValueError("d_model must be divisible by num_heads")
         self._reinit_projections(d_model, bias)
 
+    @fp32_compute()
     def forward(self, hidden_states, key_value_states, attention_mask):
         return attention_grouped([self], "cross", [hidden_states], [key_value_states], attention_mask)[0]
 
@@ -172,5 +175,6 @@ class SelfCausalAttention(BaseAttention):
             raise ValueError("d_model must be divisible by num_heads")
         self._reinit_projections(d_model, bias)
 
+    @fp32_compute()
     def forward(self, hidden_states, attention_mask):
         return attention_grouped([self], "causal", [hidden_states], None, attention_mask)[0]

@@ -226,6 +226,9 @@ class GradBuckets:
         self._step["comms"][comm.cuda_stream] = comm
 
     def _finish(self):
+        # this callback runs before the side streams' join callbacks: the deferred LayerNorm
+        # affine reductions report their parameters now
+        ops.flush_deferred_affine()
         self._launch_ready()  # the last bucket(s)
         st, self._step = self._step, None
         if st is None:

@@ -6,6 +6,7 @@ from torch import nn
 
 from .fusion import CoordinatesFusion
 from .keypoint_module import KeypointModule, joint_index_tensors, keypoint_streams_forward
+from .precision import fp32_compute
 
 
 class SCAEncoder(nn.Module):
@@ -18,6 +19,7 @@ class SCAEncoder(nn.Module):
         # model/__init__.py:96: the fusion drop rate is hard-coded to 0.2
         self.coordinates_fusion = CoordinatesFusion(cfg["in_fusion_dim"], cfg["out_fusion_dim"], 0.2)
 
+    @fp32_compute()
     def forward(self, keypoints, mask):
         """keypoints (B, T, K_all, 2), mask (B, T) -> (fuse, left, right, body) embeddings.
         The three streams run in lock-step (one launch per stage), their joint slicing

@@ -4,6 +4,7 @@ import torch.nn as nn
 
 from . import library, ops
 from .layers import drop_p, layernorm_grouped
+from .precision import fp32_compute
 
 
 def _lin(layers, xs, gelu=False, resid=None):
@@ -32,6 +33,7 @@ class CoordinatesFusion(nn.Module):
         self.inverted_res = InvertedResidual(out_feat, out_feat)
         self.drop_rate = drop_rate
 
+    @fp32_compute()
     def forward(self, left_embed, right_embed, body_embed):
         p = drop_p([self], "drop_rate")
         lo, ro, bo = _lin([self.left_se, self.right_se, self.body_se], [left_embed, right_embed, body_embed],
@@ -59,6 +61,7 @@ class InvertedResidual(nn.Module):
         self.gelu = nn.GELU()
         self.bn1 = nn.LayerNorm(in_dim)
 
+    @fp32_compute()
     def forward(self, x):
         out = _lin([self.linear_1], [x], gelu=True, resid=[x])
         out = layernorm_grouped([self.bn1], out)

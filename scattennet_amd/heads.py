@@ -20,6 +20,7 @@ from torch.autograd import Function
 from . import _lib as L
 from . import ops
 from .alignment import AlignmentModule
+from .precision import fp32_compute
 
 
 def _dev_i32(t, device):
@@ -199,6 +200,7 @@ class SeqKD(nn.Module):
         super().__init__()
         self.T = T
 
+    @fp32_compute()
     def forward(self, prediction_logits, ref_logits, use_blank=True):
         return SeqKDOp.apply(prediction_logits, ref_logits, 0 if use_blank else 1, float(self.T), 1.0,
                              float("-inf"), float("inf"))
@@ -227,6 +229,7 @@ class RecognitionHead(nn.Module):
                 nn.init.xavier_uniform_(m.weight)
                 nn.init.constant_(m.bias, 0)
 
+    @fp32_compute()
     def forward(self, left_output, right_output, fuse_output, body_output):
         heads = [self.left_gloss_classifier, self.right_gloss_classifier, self.body_gloss_classifier]
         zs = list(ops.LinearResidual.apply(3, False, left_output, right_output, body_output,

@@ -14,6 +14,7 @@ from .layers import (CoordinateMapping, FeedForward, LearningPositionEmbedding, 
                      fc1_request, ffn_grouped, pos_embed_layernorm_grouped)
 from .residual import ResidualNetwork, residual_network_grouped
 from .utils import key_padding_mask
+from .precision import fp32_compute
 
 
 # --------------------------------------------------------------------------- A9
@@ -39,6 +40,7 @@ class CoordinateAttention(nn.Module):
         self.dropout = cfg["dropout"]
         self.activation_fn = nn.GELU()
 
+    @fp32_compute(clamp=True)
     def forward(self, coord_embed, attention_mask=None):
         return coordinate_attention_grouped([self], [coord_embed], attention_mask)[0]
 
@@ -83,6 +85,7 @@ class CoordinatesMerge(nn.Module):
         self.last_layer_norm = nn.LayerNorm(cfg["d_model"])
         self.dropout = cfg["dropout"]
 
+    @fp32_compute(clamp=True)
     def forward(self, y_embed, x_embed, cross_attn_mask=None):
         return coordinates_merge_grouped([self], [y_embed], [x_embed], cross_attn_mask)[0]
 
@@ -111,6 +114,7 @@ class SeparativeCoordinateAttention(nn.Module):
         self.causal_pos_embed = LearningPositionEmbedding(cfg["max_position_embeddings"], cfg["d_model"])
         self.x_self = cfg.get("self_attn_x", True)
 
+    @fp32_compute()
     def forward(self, x_embed, y_embed, attention_mask=None, return_attn_map=False):
         outs, s_maps = sca_grouped([self], [x_embed], [y_embed], attention_mask)
         if return_attn_map:
@@ -183,6 +187,7 @@ class KeypointModule(nn.Module):
         self.sca = SeparativeCoordinateAttention(cfg)
         self.residual = ResidualNetwork(cfg["residual_blocks"])
 
+    @fp32_compute()
     def forward(self, keypoints, attention_mask=None):
         # `keypoints` is the stream's own (B, T, K, 2) slice, as MSCA_Net passes it
         idx = self.coordinate_mapping.joint_index(keypoints.device)
@@ -210,6 +215,7 @@ class KeypointStreams(nn.Module):
             self._idx = joint_index_tensors(self.streams, device)
         return self._idx
 
+    @fp32_compute()
     def forward(self, keypoints, attention_mask):
         return keypoint_streams_forward(list(self.streams), self.joint_indices(keypoints.device), keypoints,
                                         attention_mask, self.with_residual)

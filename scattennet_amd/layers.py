@@ -3,6 +3,7 @@ import torch
 from torch import nn
 
 from . import library, ops
+from .precision import fp32_compute
 
 
 class LearningPositionEmbedding(nn.Embedding):
@@ -14,6 +15,7 @@ class LearningPositionEmbedding(nn.Embedding):
         self.offset = 2
         super().__init__(num_embeddings + self.offset, embedding_dim)
 
+    @fp32_compute()
     def forward(self, inputs_embeds):
         seq_len = inputs_embeds.shape[1]
         if seq_len + self.offset > self.weight.shape[0]:
@@ -75,6 +77,7 @@ class FeedForward(nn.Module):
         self.fc2 = nn.Linear(out_dim, in_dim)
         self.dropout = dropout
 
+    @fp32_compute()
     def forward(self, x):
         return ffn_grouped([self], [x], residual=False)[0]
 
@@ -114,6 +117,7 @@ class CoordinateMapping(nn.Module):
             self._idx = torch.arange(K, dtype=torch.int32, device=device)
         return self._idx
 
+    @fp32_compute()
     def forward(self, x_coord, y_coord):
         # the kernel reads interleaved (.., K, 2) coordinates — what KeypointModule hands it
         # directly; a standalone call interleaves its two inputs first

@@ -547,7 +547,7 @@ def _ln_bwd_or_handoff(dys, vs, gam, means, rstds, lnsaved, bet):
 
     def reduce():
         reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
-    finish = (reduce, part, params)
+    finish = (reduce, part, params, (pairs, nblk, N))
     if not _LN_AFFINE_SIDE:
         reduce()
         params_produced(params)
@@ -591,7 +591,7 @@ def _ln_bwd(dys, x, gam, means, rstds, defer_affine=False, params=None):
     finish = None
     if defer_affine:  # pointers only: see _ln_bwd_or_handoff
         pairs = _ptr_pairs([(part[g], dg[g]) for g in range(G)] + [(part[g], db[g], nblk * N) for g in range(G)])
-        finish = (lambda: reduce_rows_ptr(pairs, nblk, 1, N, N, 0), part, params or ())
+        finish = (lambda: reduce_rows_ptr(pairs, nblk, 1, N, N, 0), part, params or (), (pairs, nblk, N))
     else:
         params_produced(params or ())
     return dx, dg, db, finish
@@ -842,6 +842,7 @@ def _queue_join(main, side):
 
     def _join():
         _join_pending[key] = False
+        flush_deferred_affine()
         main.wait_stream(side)
         note_join(main, side)
 
@@ -864,6 +865,35 @@ def wgrad_ready():
     return ev
 
 
+# The LayerNorm affine reductions (dgamma / dbeta from the per-block partial rows) that ride in
+# a weight-gradient side-stream section are not launched there but collected per side stream and
+# launched together once the backward has been enqueued (flush_deferred_affine: from the side
+# stream's join callback, or first thing in the data-parallel reducer's finish): one
+# reduce_rows launch for all layers instead of one ~5-us launch between every layer's weight
+# gradients.  SCA_AFFINE_DEFER=0: the per-layer launches (A/B).
+_AFFINE_DEFER = os.environ.get("SCA_AFFINE_DEFER", "1") != "0"
+_affine_pending = {}  # side stream handle -> (side stream, [(pairs, nblk, N, keep-alive tensors, params)])
+
+
+def flush_deferred_affine():
+    """Launch every collected affine reduction on the side stream it was deferred on, grouped
+    by (blocks, width), and report its parameters as produced."""
+    if not _affine_pending:
+        return
+    pend = list(_affine_pending.values())
+    _affine_pending.clear()
+    for side, entries in pend:
+        with torch.cuda.stream(side):
+            groups = {}
+            for pairs, nblk, N, _, params in entries:
+                g = groups.setdefault((nblk, N), ([], []))
+                g[0].extend(pairs)
+                g[1].extend(params)
+            for (nblk, N), (pairs, params) in groups.items():
+                reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
+                params_produced(params)
+
+
 def weight_grads(items, M=None, extra=None, ready=None):
     """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
     the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
@@ -872,18 +902,26 @@ def weight_grads(items, M=None, extra=None, ready=None):
     bias are the parameters (bias None / False: no bias gradient; True: a bias gradient
     without its parameter at hand).  bias_scale defaults to alpha; it differs when alpha
     scales the INPUT X (v from kv/2: dWv = dV^T (kv/2) but dbv = colsum(dV))."""
-    def run():
+    def run(defer=False):
         out = _weight_grads(items)
         params_produced([p for it in items for p in (it[3], it[4])])
         if extra is not None:
-            extra[0]()
-            params_produced(extra[2])
+            if defer and len(extra) > 3:
+                st = torch.cuda.current_stream()
+                pairs, nblk, N = extra[3]
+                _affine_pending.setdefault(st.cuda_stream, (st, []))[1].append(
+                    (pairs, nblk, N, list(extra[1]), list(extra[2])))
+            else:
+                extra[0]()
+                params_produced(extra[2])
         return out
 
     # a parameter that already holds a .grad gets the new gradient added by autograd as soon
-    # as this returns (ordered on the current stream only): compute on the current stream
+    # as this returns (ordered on the current stream only), and so does a non-leaf parameter
+    # view (precision.fp32_compute's p.float(): its cast backward reads the gradient at once):
+    # compute on the current stream
     params = [it[3] for it in items] + list(extra[2] if extra is not None else ())
-    if not _WGRAD_SIDE or _LIBRARY_MODE or any(p.grad is not None for p in params):
+    if not _WGRAD_SIDE or _LIBRARY_MODE or any(not p.is_leaf or p.grad is not None for p in params):
         return run()
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
@@ -899,7 +937,7 @@ def weight_grads(items, M=None, extra=None, ready=None):
     for t in (extra[1] if extra is not None else ()):
         t.record_stream(side)
     with torch.cuda.stream(side):
-        out = run()
+        out = run(defer=_AFFINE_DEFER)
     _queue_join(main, side)
     return out
 

@@ -7,6 +7,7 @@ import torch.nn as nn
 
 from . import library, ops
 from .layers import layernorm_grouped
+from .precision import fp32_compute
 
 
 class ResidualBlock(nn.Module):
@@ -28,6 +29,7 @@ class ResidualBlock(nn.Module):
         if self.downsample:
             self.pool = nn.MaxPool1d(kernel_size=2, stride=2)
 
+    @fp32_compute()
     def forward(self, x):
         return residual_block_grouped([self], [x])[0]
 
@@ -57,6 +59,7 @@ class PermuteLayer(nn.Module):
         super().__init__()
         self.dims = dims
 
+    @fp32_compute()
     def forward(self, x):
         return x.permute(*self.dims)
 
@@ -90,6 +93,7 @@ class ResidualNetwork(nn.Module):
                 else:
                     self.shortcuts.append(None)
 
+    @fp32_compute()
     def forward(self, x):
         outs = residual_network_grouped([self], [x], return_all=True)
         return outs[0][-1], outs[0]
