@@ -875,9 +875,38 @@ _AFFINE_DEFER = os.environ.get("SCA_AFFINE_DEFER", "1") != "0"
 _affine_pending = {}  # side stream handle -> (side stream, [(pairs, nblk, N, keep-alive tensors, params)])
 
 
+_flush_queued = [False]
+_AFFINE_DEFER_MAX = 256 * 512  # partial-row floats per problem up to which a LayerNormAdd defers
+
+
+def _affine_deferrable(params):
+    """Whether a LayerNorm's dgamma / dbeta reduction may be deferred to the end of the backward:
+    autograd takes the (not yet written) gradient tensors over as .grad, which is safe only
+    for leaf parameters without a .grad to add to."""
+    return _AFFINE_DEFER and not _LIBRARY_MODE and all(p.is_leaf and p.grad is None for p in params)
+
+
+def _affine_finish(part, dg, db, nblk, N, params, defer):
+    """dgamma / dbeta = fixed-order sums of the per-block partial rows: now, or (defer) collected
+    on the current stream and launched with the other deferred reductions by
+    flush_deferred_affine, which a final backward callback runs at the latest."""
+    G = len(part)
+    pairs = _ptr_pairs([(part[g], dg[g]) for g in range(G)] + [(part[g], db[g], nblk * N) for g in range(G)])
+    if not defer:
+        reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
+        params_produced(params)
+        return
+    st = torch.cuda.current_stream()
+    _affine_pending.setdefault(st.cuda_stream, (st, []))[1].append((pairs, nblk, N, list(part), list(params)))
+    if not _flush_queued[0]:
+        _flush_queued[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(flush_deferred_affine)
+
+
 def flush_deferred_affine():
     """Launch every collected affine reduction on the side stream it was deferred on, grouped
     by (blocks, width), and report its parameters as produced."""
+    _flush_queued[0] = False
     if not _affine_pending:
         return
     pend = list(_affine_pending.values())
@@ -1708,10 +1737,13 @@ class LayerNormAdd(Function):
         dpost = [torch.empty_like(t) for t in x] if ctx.has_post else [None] * G
         dg = [param_grad_empty(t) for t in gam]
         db = [param_grad_empty(t) for t in ctx.bet]
-        if hs is not None:  # dL/dv (= dL/dx) done; the dgamma / dbeta partials summed here
+        params = list(gam) + list(ctx.bet)
+        # deferred when the partial rows are few (config 2 / 3: +0.5-0.7 %); config 5's 1024 x 512
+        # partials per problem reduce better beside the weight gradients where they fall (-0.4 %
+        # deferred; profiles/r05_misc/affine_defer2_ab.txt)
+        defer = _affine_deferrable(params) and L.lib().sca_layernorm_bwd_blocks(rows) * N <= _AFFINE_DEFER_MAX
+        if hs is not None:  # dL/dv (= dL/dx) done; the dgamma / dbeta partials summed below
             dx, part, nblk = [h[2] for h in hs], [h[3] for h in hs], hs[0][4]
-            reduce_rows([(part[g], dg[g], 1.0) for g in range(G)] +
-                        [(part[g][nblk * N:], db[g], 1.0) for g in range(G)], nblk, 1, N, N, 0)
         else:
             nblk = L.lib().sca_layernorm_bwd_blocks(rows)
             dx = [torch.empty_like(t) for t in x]
@@ -1722,11 +1754,15 @@ class LayerNormAdd(Function):
                                                                     gam[g].data_ptr(), means[g].data_ptr(),
                                                                     rstds[g].data_ptr(), ptr(ys[g]), act,
                                                                     ptr(dpost[g]), dx[g].data_ptr(),
-                                                                    dg[g].data_ptr(), db[g].data_ptr(),
+                                                                    None if defer else dg[g].data_ptr(),
+                                                                    None if defer else db[g].data_ptr(),
                                                                     part[g].data_ptr()) for g in gs])
                 L.check(L.lib().sca_layernorm_bwd(len(gs), arr, rows, N, ctx.r_mod, ctx.r_off, 0,
                                                   L.stream_handle()), "sca_layernorm_bwd")
-        params_produced(list(gam) + list(ctx.bet))
+        if hs is not None or defer:
+            _affine_finish(part, dg, db, nblk, N, params, defer)
+        else:
+            params_produced(params)
         dtab = []
         if pos:
             B, T = x[0].shape[0], x[0].shape[1]
