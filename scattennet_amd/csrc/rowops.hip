@@ -271,13 +271,61 @@ __global__ __launch_bounds__(256) void reduce_rows_few_kernel(const ReduceArgs a
   st4(o, t);
 }
 
+// Many rows (S > 16, e.g. the LayerNorm dgamma / dbeta partials: one row per row block), float4
+// columns: a workgroup takes 64 columns; lane (cg = lane & 15, rq = lane >> 4) of wave w owns
+// float4 column group cg and row residue rs = 4w + rq (mod 64), summing its rows with 8 loads of
+// 16 B in flight (128 KB per workgroup in flight, against 32 KB for the scalar form: the sum is
+// latency-bound).  The 64 residues' partials are added in order through LDS (deterministic).
+__global__ __launch_bounds__(1024) void reduce_rows_vec_kernel(const ReduceArgs a) {
+  const sca_reduce_problem& P = a.p[blockIdx.z];
+  __shared__ __attribute__((aligned(16))) float red[64][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cg = lane & 15, rs = 4 * w + (lane >> 4);
+  const int j = blockIdx.x * 64 + 4 * cg;
+  const int i = blockIdx.y;
+  f32x4 acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (j < a.N) {
+    const float* base = P.in + (long)i * a.stride_i + j;
+    // up to 8 independent loads per round, the last round predicated (S = 256: all 4 at once)
+    for (int s = rs; s < a.S; s += 8 * 64) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s + 64 * u < a.S) acc[u] += ld4(base + (long)(s + 64 * u) * a.stride_s);
+    }
+  }
+  st4(&red[rs][4 * cg], ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])));
+  __syncthreads();
+  if (threadIdx.x < 64 && blockIdx.x * 64 + (int)threadIdx.x < a.N) {
+    const int c = threadIdx.x;
+    float t = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) t += red[k][c];
+    t *= P.scale;
+    float* o = P.out + (long)i * a.N + blockIdx.x * 64 + c;
+    if (a.accumulate) t += *o;
+    *o = t;
+  }
+}
+
+// SCA_REDUCE_VEC=0: the scalar form for every S > 16 (A/B)
+bool reduce_vec_on() {
+  static const bool on = !(getenv("SCA_REDUCE_VEC") && atoi(getenv("SCA_REDUCE_VEC")) == 0);
+  return on;
+}
+
 int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
-  bool few = a.S <= RED_WAVES && (a.N & 3) == 0 && (a.stride_s & 3) == 0 && (a.stride_i & 3) == 0;
-  for (int i = 0; few && i < nprob; ++i)
-    few = !((reinterpret_cast<uintptr_t>(a.p[i].in) | reinterpret_cast<uintptr_t>(a.p[i].out)) & 15);
-  if (few) {
+  const bool vec_ok = (a.N & 3) == 0 && (a.stride_s & 3) == 0 && (a.stride_i & 3) == 0;
+  bool aligned = true;
+  for (int i = 0; i < nprob; ++i)
+    aligned = aligned && !((reinterpret_cast<uintptr_t>(a.p[i].in) | reinterpret_cast<uintptr_t>(a.p[i].out)) & 15);
+  if (vec_ok && aligned && a.S <= RED_WAVES) {
     dim3 grid((a.N / 4 + 255) / 256, a.I, nprob);
     hipLaunchKernelGGL(reduce_rows_few_kernel, grid, dim3(256), 0, st, a);
+  } else if (vec_ok && aligned && reduce_vec_on()) {
+    dim3 grid((a.N + 63) / 64, a.I, nprob);
+    hipLaunchKernelGGL(reduce_rows_vec_kernel, grid, dim3(1024), 0, st, a);
   } else {
     dim3 grid((a.N + 63) / 64, a.I, nprob);
     hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(1024), 0, st, a);
