@@ -271,50 +271,6 @@ __global__ __launch_bounds__(256) void reduce_rows_few_kernel(const ReduceArgs a
   st4(o, t);
 }
 
-// Many rows (S > 16, e.g. the LayerNorm dgamma / dbeta partials: one row per row block), float4
-// columns: a workgroup takes 64 columns; lane (cg = lane & 15, rq = lane >> 4) of wave w owns
-// float4 column group cg and row residue rs = 4w + rq (mod 64), summing its rows with 8 loads of
-// 16 B in flight (128 KB per workgroup in flight, against 32 KB for the scalar form: the sum is
-// latency-bound).  The 64 residues' partials are added in order through LDS (deterministic).
-__global__ __launch_bounds__(1024) void reduce_rows_vec_kernel(const ReduceArgs a) {
-  const sca_reduce_problem& P = a.p[blockIdx.z];
-  __shared__ __attribute__((aligned(16))) float red[64][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int cg = lane & 15, rs = 4 * w + (lane >> 4);
-  const int j = blockIdx.x * 64 + 4 * cg;
-  const int i = blockIdx.y;
-  f32x4 acc[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (j < a.N) {
-    const float* base = P.in + (long)i * a.stride_i + j;
-    // up to 8 independent loads per round, the last round predicated (S = 256: all 4 at once)
-    for (int s = rs; s < a.S; s += 8 * 64) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (s + 64 * u < a.S) acc[u] += ld4(base + (long)(s + 64 * u) * a.stride_s);
-    }
-  }
-  st4(&red[rs][4 * cg], ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])));
-  __syncthreads();
-  if (threadIdx.x < 64 && blockIdx.x * 64 + (int)threadIdx.x < a.N) {
-    const int c = threadIdx.x;
-    float t = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < 64; ++k) t += red[k][c];
-    t *= P.scale;
-    float* o = P.out + (long)i * a.N + blockIdx.x * 64 + c;
-    if (a.accumulate) t += *o;
-    *o = t;
-  }
-}
-
-// SCA_REDUCE_VEC=0: the scalar form for every S > 16 (A/B)
-bool reduce_vec_on() {
-  static const bool on = !(getenv("SCA_REDUCE_VEC") && atoi(getenv("SCA_REDUCE_VEC")) == 0);
-  return on;
-}
-
 int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
   const bool vec_ok = (a.N & 3) == 0 && (a.stride_s & 3) == 0 && (a.stride_i & 3) == 0;
   bool aligned = true;
@@ -323,9 +279,6 @@ int launch_reduce(const ReduceArgs& a, int nprob, hipStream_t st) {
   if (vec_ok && aligned && a.S <= RED_WAVES) {
     dim3 grid((a.N / 4 + 255) / 256, a.I, nprob);
     hipLaunchKernelGGL(reduce_rows_few_kernel, grid, dim3(256), 0, st, a);
-  } else if (vec_ok && aligned && reduce_vec_on()) {
-    dim3 grid((a.N + 63) / 64, a.I, nprob);
-    hipLaunchKernelGGL(reduce_rows_vec_kernel, grid, dim3(1024), 0, st, a);
   } else {
     dim3 grid((a.N + 63) / 64, a.I, nprob);
     hipLaunchKernelGGL(reduce_rows_kernel, grid, dim3(1024), 0, st, a);
@@ -628,39 +581,58 @@ __device__ __forceinline__ void gather_coords(float (*xs)[MAP_KMAX], float (*ys)
   }
 }
 
+// The weights (N x K row-major, K = the stream's joint count: rows not float4-aligned) are
+// staged through LDS in chunks of MAP_KC joints, transposed to [joint][column]: the chunk is
+// read with consecutive lanes on consecutive joints of one weight row (64-B runs), where a
+// thread reading its own row touched one cache line per lane per load; each thread then reads
+// its column conflict-free.  Same k order per output: bit-identical to the direct form.
+constexpr int MAP_KC = 16, MAP_WLD = 257;
 __global__ __launch_bounds__(256) void coord_map_fwd_kernel(const MapArgs a) {
   const sca_coord_map_problem& P = a.p[blockIdx.y];
   __shared__ float xs[MAP_ROWS][MAP_KMAX], ys[MAP_ROWS][MAP_KMAX];
+  __shared__ float wsx[MAP_KC][MAP_WLD], wsy[MAP_KC][MAP_WLD];
   const int row0 = blockIdx.x * MAP_ROWS;
   const int K = P.K;
   gather_coords(xs, ys, P.kp, P.idx, K, a.K_all, row0, MAP_ROWS, a.rows);
-  __syncthreads();
-  for (int n = threadIdx.x; n < a.N; n += 256) {
+  for (int n0 = 0; n0 < a.N; n0 += 256) {
+    const int n = n0 + threadIdx.x;
     float ax[MAP_ROWS], ay[MAP_ROWS];
 #pragma unroll
     for (int r = 0; r < MAP_ROWS; ++r) ax[r] = ay[r] = 0.f;
-    const float* wxr = P.wx + (long)n * K;
-    const float* wyr = P.wy + (long)n * K;
-    // the weight row (K floats, no float4 alignment) in chunks of 8 loads issued together:
-    // one L2 round trip per 8 joints instead of one per joint (same k order: bit-identical)
-    for (int k0 = 0; k0 < K; k0 += 8) {
-      float wx[8], wy[8];
+    for (int k0 = 0; k0 < K; k0 += MAP_KC) {
+      __syncthreads();  // the previous chunk consumed (first pass: the gather landed)
+      // every load of the chunk issued before any is used: addresses past the weight are
+      // clamped to its last element (always valid) and their values zeroed by a select
+      constexpr int PER = 256 * MAP_KC / 256;
+      float vx[PER], vy[PER];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = min(k0 + j, K - 1);
-        wx[j] = wxr[k];
-        wy[j] = wyr[k];
+      for (int i = 0; i < PER; ++i) {
+        const int e = threadIdx.x + 256 * i, nn = e / MAP_KC, kk = e % MAP_KC;
+        const long off = min((long)(n0 + nn) * K + k0 + kk, (long)a.N * K - 1);
+        vx[i] = P.wx[off];
+        vy[i] = P.wy[off];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (k0 + j >= K) break;  // wave-uniform
+      for (int i = 0; i < PER; ++i) {
+        const int e = threadIdx.x + 256 * i, nn = e / MAP_KC, kk = e % MAP_KC;
+        const bool in = n0 + nn < a.N && k0 + kk < K;
+        wsx[kk][nn] = in ? vx[i] : 0.f;
+        wsy[kk][nn] = in ? vy[i] : 0.f;
+      }
+      __syncthreads();
+      const int kc = min(MAP_KC, K - k0);
+#pragma unroll
+      for (int j = 0; j < MAP_KC; ++j) {
+        if (j >= kc) break;  // wave-uniform
+        const float wx = wsx[j][threadIdx.x], wy = wsy[j][threadIdx.x];
 #pragma unroll
         for (int r = 0; r < MAP_ROWS; ++r) {
-          ax[r] = fmaf(xs[r][k0 + j], wx[j], ax[r]);
-          ay[r] = fmaf(ys[r][k0 + j], wy[j], ay[r]);
+          ax[r] = fmaf(xs[r][k0 + j], wx, ax[r]);
+          ay[r] = fmaf(ys[r][k0 + j], wy, ay[r]);
         }
       }
     }
+    if (n >= a.N) continue;
     const float bx = P.bx ? P.bx[n] : 0.f, by = P.by ? P.by[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < MAP_ROWS; ++r) {

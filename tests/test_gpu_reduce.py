@@ -1,7 +1,7 @@
 """sca_reduce_rows (the fixed-order row sums behind every bias / LayerNorm-affine / position-table
-gradient) at kernel level against float64 sums: the few-row form (S <= 16), the float4 many-row
-form (S > 16, N % 4 == 0) and the scalar form (N % 4 != 0), with a row stride, several column
-blocks (I), a scale and accumulation; repeated launches are bit-identical (fixed order)."""
+gradient) at kernel level against float64 sums: the few-row float4 form (S <= 16, N % 4 == 0)
+and the 16-wave form (more rows, or N % 4 != 0), with a row stride, several column blocks (I), a
+scale and accumulation; repeated launches are bit-identical (fixed order)."""
 import pytest
 import torch
 
