@@ -39,11 +39,18 @@ def _linear(layers, xs):
     return list(library.linear_apply(G, False, *xs, *[l.weight for l in layers], *[l.bias for l in layers]))
 
 
+_FAN_OUT_X = True  # A/B (tools/bench_var.py): the block input's two gradients summed by autograd
+
+
 def residual_block_grouped(blocks, xs):
     """out = relu(norm2(linear2(relu(norm1(linear1 x)))) + proj?(x)); then MaxPool over T."""
     b0 = blocks[0]
-    r = _linear([b.projection for b in blocks], xs) if b0.need_projection else xs
-    h = _linear([b.linear1 for b in blocks], xs)
+    # x has two consumers (linear1 and the projection / the identity residual of norm2): one
+    # fan-out, so that its two gradients are summed in one grouped launch for all streams
+    # instead of one autograd add per stream
+    x_lin, x_res = ops.fan_out(xs, 2) if _FAN_OUT_X and not library.compiling() else (xs, xs)
+    r = _linear([b.projection for b in blocks], x_res) if b0.need_projection else x_res
+    h = _linear([b.linear1 for b in blocks], x_lin)
     h = layernorm_grouped([b.norm1 for b in blocks], h, relu=True)
     h = _linear([b.linear2 for b in blocks], h)
     h = layernorm_grouped([b.norm2 for b in blocks], h, post=r, relu=True)
