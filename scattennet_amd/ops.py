@@ -875,7 +875,7 @@ _AFFINE_DEFER = os.environ.get("SCA_AFFINE_DEFER", "1") != "0"
 _affine_pending = {}  # side stream handle -> (side stream, [(pairs, nblk, N, keep-alive tensors, params)])
 
 
-_flush_queued = [False]
+_flush_queued = [None]  # the autograd graph task whose final callbacks hold a flush
 _AFFINE_DEFER_MAX = 256 * 512  # partial-row floats per problem up to which a LayerNormAdd defers
 
 
@@ -898,15 +898,16 @@ def _affine_finish(part, dg, db, nblk, N, params, defer):
         return
     st = torch.cuda.current_stream()
     _affine_pending.setdefault(st.cuda_stream, (st, []))[1].append((pairs, nblk, N, list(part), list(params)))
-    if not _flush_queued[0]:
-        _flush_queued[0] = True
+    task = torch._C._current_graph_task_id()  # one flush callback per backward (a backward that
+    if _flush_queued[0] != task:               # raised before its callbacks leaves no stale flag)
+        _flush_queued[0] = task
         torch.autograd.Variable._execution_engine.queue_callback(flush_deferred_affine)
 
 
 def flush_deferred_affine():
     """Launch every collected affine reduction on the side stream it was deferred on, grouped
     by (blocks, width), and report its parameters as produced."""
-    _flush_queued[0] = False
+    _flush_queued[0] = None
     if not _affine_pending:
         return
     pend = list(_affine_pending.values())
