@@ -836,12 +836,13 @@ def note_join(into, child):
 
 def _queue_join(main, side):
     key = (main.cuda_stream, side.cuda_stream)
-    if _join_pending.get(key):
+    task = torch._C._current_graph_task_id()  # one join per backward (keyed by the graph task, so
+    if _join_pending.get(key) == task:         # a backward that raised leaves no stale entry)
         return
-    _join_pending[key] = True
+    _join_pending[key] = task
 
     def _join():
-        _join_pending[key] = False
+        _join_pending[key] = None
         flush_deferred_affine()
         main.wait_stream(side)
         note_join(main, side)
@@ -873,6 +874,7 @@ def wgrad_ready():
 # gradients.  SCA_AFFINE_DEFER=0: the per-layer launches (A/B).
 _AFFINE_DEFER = os.environ.get("SCA_AFFINE_DEFER", "1") != "0"
 _affine_pending = {}  # side stream handle -> (side stream, [(pairs, nblk, N, keep-alive tensors, params)])
+_affine_task = None  # the autograd graph task the pending entries belong to
 
 
 _flush_queued = [None]  # the autograd graph task whose final callbacks hold a flush
@@ -896,12 +898,22 @@ def _affine_finish(part, dg, db, nblk, N, params, defer):
         reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
         params_produced(params)
         return
-    st = torch.cuda.current_stream()
-    _affine_pending.setdefault(st.cuda_stream, (st, []))[1].append((pairs, nblk, N, list(part), list(params)))
+    _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(part), list(params)))
     task = torch._C._current_graph_task_id()  # one flush callback per backward (a backward that
     if _flush_queued[0] != task:               # raised before its callbacks leaves no stale flag)
         _flush_queued[0] = task
         torch.autograd.Variable._execution_engine.queue_callback(flush_deferred_affine)
+
+
+def _affine_defer(st, entry):
+    """Collect one deferred reduction on stream st.  Entries left by a backward that raised
+    before its final callbacks (their gradients are void) are dropped, never launched later."""
+    global _affine_task
+    task = torch._C._current_graph_task_id()
+    if task != _affine_task:
+        _affine_pending.clear()
+        _affine_task = task
+    _affine_pending.setdefault(st.cuda_stream, (st, []))[1].append(entry)
 
 
 def flush_deferred_affine():
@@ -937,10 +949,8 @@ def weight_grads(items, M=None, extra=None, ready=None):
         params_produced([p for it in items for p in (it[3], it[4])])
         if extra is not None:
             if defer and len(extra) > 3:
-                st = torch.cuda.current_stream()
                 pairs, nblk, N = extra[3]
-                _affine_pending.setdefault(st.cuda_stream, (st, []))[1].append(
-                    (pairs, nblk, N, list(extra[1]), list(extra[2])))
+                _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(extra[1]), list(extra[2])))
             else:
                 extra[0]()
                 params_produced(extra[2])
