@@ -101,17 +101,36 @@ class GradBuckets:
         return torch.cuda.current_stream() if self.params[0].is_cuda else None
 
     def _begin(self):
-        """First sink call of a backward: choose this step's mode and queue its finish."""
+        """First sink call of a backward: choose this step's mode and queue its finish.  A step
+        left by a backward that raised before its finish callback is drained first: its issued
+        all-reduces (the same on every rank) complete before this step writes the buckets
+        again; its not yet issued ones are dropped."""
+        stale = self._step
+        if stale is not None:
+            for work in stale["works"]:
+                work.wait()
+            cur = self._stream()
+            if cur is not None:
+                for comm in stale["comms"].values():
+                    cur.wait_stream(comm)
+                    ops.note_join(cur, comm)
         fast = self.plan is not None and all(self.params[i].grad is None for i in self.slot)
-        self._step = {"fast": fast, "pending": [len(b[2]) for b in self.plan] if fast else None,
+        self._step = {"task": torch._C._current_graph_task_id(),
+                      "fast": fast, "pending": [len(b[2]) for b in self.plan] if fast else None,
                       "streams": [dict() for _ in self.plan] if fast else None, "works": [],
                       "seen": set(), "producers": {}, "comms": {}, "ready": []}
         torch.autograd.Variable._execution_engine.queue_callback(self._finish)
 
     # ------------------------------------------------------------------ sink protocol (ops)
-    def grad_buffer(self, p):
-        if self._step is None:
+    def _current(self):
+        """This backward's step state: begun at its first sink call.  A state left by a backward
+        that raised before its finish callback (another autograd graph task) is discarded."""
+        if self._step is None or self._step["task"] != torch._C._current_graph_task_id():
             self._begin()
+        return self._step
+
+    def grad_buffer(self, p):
+        self._current()
         if not self._step["fast"]:
             return None
         i = self._index(p)
@@ -121,9 +140,7 @@ class GradBuckets:
         return self.flat[o:o + n].view(p.shape)
 
     def produced(self, params):
-        if self._step is None:
-            self._begin()
-        st = self._step
+        st = self._current()
         self._launch_ready()  # buckets completed at the previous report
         stream = self._stream()
         if stream is not None:

@@ -121,9 +121,48 @@ def main_sink(out_path):
         torch.save(results, out_path)
 
 
+def main_sink_raise(out_path):
+    """Discovery and a bucketed step, then a backward that raises at its very end (a hook on
+    the input: every bucket's all-reduce is already issued, the finish callback never runs),
+    then a clean bucketed step: its gradients must be exact."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ps, unused = sink_model()
+    red = GradBuckets(ps + [unused], world, bucket_mb=1024 * 4 / 2 ** 20, overlap=True)
+    sl = slice(rank * 8 // world, (rank + 1) * 8 // world)
+    for step in range(2):
+        x, gy = sink_data(step)
+        for p in ps:
+            p.grad = None
+        sink_forward(ps, x[sl]).backward(gy[sl])
+        red.sync()
+
+    def boom(_):
+        raise RuntimeError("boom")
+
+    x, gy = sink_data(5)
+    xs = x[sl].clone().requires_grad_(True)
+    xs.register_hook(boom)
+    for p in ps:
+        p.grad = None
+    raised = False
+    try:
+        sink_forward(ps, xs).backward(gy[sl])
+    except RuntimeError:
+        raised = True
+    x, gy = sink_data(2)
+    for p in ps:
+        p.grad = None
+    sink_forward(ps, x[sl]).backward(gy[sl])
+    red.sync()
+    results = {"raised": raised, "after": [p.grad.clone() for p in ps]}
+    red.close()
+    if rank == 0:
+        torch.save(results, out_path)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(1)
     dist.init_process_group("gloo")
-    (main_sink if sys.argv[2] == "sink" else main_oracle)(sys.argv[1])
+    {"sink": main_sink, "sink_raise": main_sink_raise}.get(sys.argv[2], main_oracle)(sys.argv[1])
     dist.barrier()
     dist.destroy_process_group()

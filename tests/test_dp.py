@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _launch(out, mode):
-    port = str(29500 + (os.getpid() + (7 if mode == "sink" else 0)) % 2000)
+    port = str(29500 + (os.getpid() + {"sink": 7, "sink_raise": 13}.get(mode, 0)) % 2000)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", port, os.path.join(ROOT, "tests", "dp_worker.py"),
            str(out), mode]
@@ -60,3 +60,17 @@ def test_bucketed_reducer_matches_full_batch(tmp_path):
     assert got["step1_slot"] == [True, True, False, False, True, True, True, True]
     assert not any(got["step0_slot"])  # discovery step: plain allocations
     assert len(got["buckets"]) >= 2 and got["unused_grad_none"]
+
+
+def test_bucketed_reducer_recovers_from_a_raised_backward(tmp_path):
+    """A backward that raised before the reducer's finish (its all-reduces issued, never
+    joined) is drained at the next backward's first sink call; the next step is exact."""
+    got = _launch(tmp_path / "r.pt", "sink_raise")
+    assert got["raised"]
+    ps, _ = DW.sink_model()
+    x, gy = DW.sink_data(2)
+    y = DW.sink_forward(ps, x)
+    y.backward(gy / 2)
+    for i, (a, p) in enumerate(zip(got["after"], ps)):
+        b = p.grad
+        assert float((a - b).abs().max()) <= 1e-5 * (float(b.abs().max()) + 1e-6), i
