@@ -1014,8 +1014,12 @@ def _weight_grads(items):
                 # 46): 6-20 % faster than both the LDS-DMA k-split (36) and the plain LDS-DMA
                 # kernel at every config-2 / 3 shape (tools/tn_library_compare.py,
                 # profiles/r05_tn/tnr_compare_*.log); split 2, or 4 when that makes exactly one
-                # full round of three workgroups per CU with >= 512 rows per split
-                tile, sk = 46, (4 if tiles * 4 == 768 and Kr >= 2048 else (2 if Kr >= 512 else 1))
+                # full round of three workgroups per CU with >= 512 rows per split and the
+                # problems are FFN-sized (config 2's 4 x (768, 256): +0.6 % in step over 2); the
+                # many small problems of config 3's attention (12 x (256, 256)) run better at 2
+                # in step (+1.1 %, profiles/r05_misc/tnr_split_rule_ab.txt) though 4 is faster alone
+                big = all(items[i][3].shape[0] * items[i][3].shape[1] >= 768 * 256 for i in sub)
+                tile, sk = 46, (4 if tiles * 4 == 768 and Kr >= 2048 and big else (2 if Kr >= 512 else 1))
                 if _TNR_SK and Kr // _TNR_SK >= 256:
                     sk = _TNR_SK
             elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
