@@ -642,10 +642,18 @@ _TNB_MIN_K = int(os.environ.get("SCA_TNB_MIN_K", "4096"))  # A/B switch (0: neve
 _TNB_RATE2, _TNB_RATE1, _TNB_EPI = 0.86, 0.88, 3.0
 
 
+_TNB_MODEL = os.environ.get("SCA_TNB_MODEL", "0") != "0"  # A/B: the isolated-speed split model
+
+
 def _tnb_split(K, tiles128):
-    """Split-K for tile 43: the split whose estimated per-CU time is least — workgroups dealt
-    over 256 CUs, two at a time at _TNB_RATE2, a leftover one at _TNB_RATE1, plus an epilogue
-    cost per workgroup (ties: the smaller split, fewer slabs)."""
+    """Split-K for tile 43.  In the step: 1 — one long workgroup per output tile, the fewest
+    workgroups holding CUs beside the critical chain (config 5: +0.5 % over the model below,
+    whose FFN choice of split 4 is faster alone; profiles/r05_misc/tnb_split_cfg5_ab.txt).
+    SCA_TNB_MODEL=1: the split whose estimated per-CU time is least — workgroups dealt over
+    256 CUs, two at a time at _TNB_RATE2, a leftover one at _TNB_RATE1, plus an epilogue cost
+    per workgroup (ties: the smaller split, fewer slabs)."""
+    if not _TNB_MODEL:
+        return 1
     best, best_sk = None, 1
     for sk in range(1, _SPLITK_MAX + 1):
         if sk > 1 and K // sk < 1024:
