@@ -419,6 +419,24 @@ typedef struct {
 #define SCA_DROPOUT_MAX_PROBLEMS 12
 int sca_dropout(int nprob, const sca_dropout_problem* probs, long rows, int cols, float p, void* stream);
 
+/* Key validity of the (B, T) attention mask the SCA stack receives, as the (B, T) fp32 1/0
+ * vector the attention kernels read (key_valid):
+ *   key_valid[i] = ((float)mask[i] == 1.0f) ? 1 : 0
+ * — the reference's predicate: create_attention_mask / create_causal_attention_mask
+ * (model/utils.py:8-12, 19-23) cast the mask to fp32 and mask every key where
+ * 1.0 - mask != 0, so only the value 1 keeps a key (2, 0.5, -1, NaN all mask it).
+ * dtype: the mask's element type (SCA_MASK_*); any alignment; n = 0 is a no-op.        */
+#define SCA_MASK_F32 0
+#define SCA_MASK_F64 1
+#define SCA_MASK_I64 2
+#define SCA_MASK_I32 3
+#define SCA_MASK_U8 4   /* bool / uint8 */
+#define SCA_MASK_F16 5
+#define SCA_MASK_BF16 6
+#define SCA_MASK_I8 7
+#define SCA_MASK_I16 8
+int sca_key_valid(const void* mask, int dtype, float* key_valid, long n, void* stream);
+
 /* Registers a device-resident step counter (or NULL) read by every dropout mask at run
  * time: effective seed = seed + counter * 0x9E3779B97F4A7C15.  A hipGraph that captures
  * the counter's increment then draws fresh masks on every replay although the seeds in

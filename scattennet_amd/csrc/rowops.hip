@@ -856,6 +856,34 @@ __global__ __launch_bounds__(256) void dropout_kernel(const DropArgs a) {
     P.y[e] = dm.apply((uint32_t)e, P.x[e]);
 }
 
+// ------------------------------------------------------------------------------ key validity
+// (model/utils.py:8-12, 19-23: 1.0 - mask.to(fp32) masks every non-zero, so only 1 keeps)
+struct KeyValidArgs {
+  const void* mask;
+  float* out;
+  long n;
+  int dtype;
+};
+
+__device__ __forceinline__ float mask_value(const void* m, int dtype, long i) {
+  switch (dtype) {
+    case SCA_MASK_F64: return (float)static_cast<const double*>(m)[i];
+    case SCA_MASK_I64: return (float)static_cast<const long long*>(m)[i];
+    case SCA_MASK_I32: return (float)static_cast<const int*>(m)[i];
+    case SCA_MASK_U8: return (float)static_cast<const unsigned char*>(m)[i];
+    case SCA_MASK_F16: return (float)static_cast<const _Float16*>(m)[i];
+    case SCA_MASK_BF16: return __uint_as_float((uint32_t)static_cast<const unsigned short*>(m)[i] << 16);
+    case SCA_MASK_I8: return (float)static_cast<const signed char*>(m)[i];
+    case SCA_MASK_I16: return (float)static_cast<const short*>(m)[i];
+    default: return static_cast<const float*>(m)[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void key_valid_kernel(const KeyValidArgs a) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (long)gridDim.x * 256)
+    a.out[i] = mask_value(a.mask, a.dtype, i) == 1.f ? 1.f : 0.f;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------ C ABI
@@ -1141,6 +1169,20 @@ extern "C" int sca_dropout(int nprob, const sca_dropout_problem* probs, long row
   const int blocks = (int)(want < 2048 ? (want > 0 ? want : 1) : 2048);
   hipLaunchKernelGGL(dropout_kernel, dim3(blocks, nprob), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_dropout: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
+extern "C" int sca_key_valid(const void* mask, int dtype, float* key_valid, long n, void* stream) {
+  if (n < 0 || dtype < SCA_MASK_F32 || dtype > SCA_MASK_I16 || (n > 0 && (!mask || !key_valid))) {
+    sca_set_error("sca_key_valid: bad arguments (dtype must be one of SCA_MASK_*)");
+    return SCA_ERR_ARG;
+  }
+  if (n == 0) return SCA_OK;
+  const long want = (n + 255) / 256;
+  const int blocks = (int)(want < 1024 ? want : 1024);
+  hipLaunchKernelGGL(key_valid_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     KeyValidArgs{mask, key_valid, n, dtype});
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_key_valid: launch failed"); return SCA_ERR_LAUNCH; }
   return SCA_OK;
 }
 

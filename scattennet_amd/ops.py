@@ -1141,6 +1141,26 @@ def _attn_bwd_kernel_name(hd, am, causal, drop, Tq, Tk, dq_part):
     return f"attn_bwd_dq_kernel<{hd}, {tf(am)}, {tf(causal)}, {tf(drop)}>"
 
 
+_MASK_DTYPES = {torch.float32: 0, torch.float64: 1, torch.int64: 2, torch.int32: 3, torch.bool: 4, torch.uint8: 4,
+                torch.float16: 5, torch.bfloat16: 6, torch.int8: 7, torch.int16: 8}
+
+
+def key_valid_vector(mask):
+    """(B, T) mask of any integer / bool / float dtype -> (B, T) fp32 1/0 key validity with the
+    reference's predicate (kept iff the fp32 value equals 1; sca_key_valid)."""
+    code = _MASK_DTYPES.get(mask.dtype)
+    if code is None:
+        raise TypeError(f"attention mask dtype {mask.dtype} is not supported")
+    if not mask.is_cuda or torch.compiler.is_compiling():
+        # the same predicate as an expression torch.compile can trace (and for a mask built on
+        # the CPU: the attention launches that read it refuse CPU tensors themselves)
+        return (mask.to(torch.float32) == 1).to(torch.float32)
+    m = mask.contiguous()
+    out = torch.empty(mask.shape, dtype=torch.float32, device=mask.device)
+    L.check(L.lib().sca_key_valid(m.data_ptr(), code, out.data_ptr(), m.numel(), L.stream_handle()), "sca_key_valid")
+    return out
+
+
 class KeyPaddingMask:
     """The SCA mask contract without the B*T^2 materialisation: per-clip key validity
     (B, Tk) as fp32 1/0 plus the causal flags.  Semantically identical to the additive masks
@@ -1151,9 +1171,9 @@ class KeyPaddingMask:
             raise ValueError("key padding mask must be (B, T)")
         self.mask = mask
         self.causal_plus_one = causal_plus_one
-        # one comparison kernel writing fp32 directly (the `!= 0` then `.to` pair was two launches)
-        self.key_valid = torch.empty(mask.shape, dtype=torch.float32, device=mask.device)
-        torch.ne(mask, 0, out=self.key_valid)
+        # the reference keeps a key only where mask == 1 (model/utils.py:8-12: 1.0 - mask is
+        # masked wherever non-zero), written as fp32 1/0 by one sca_key_valid launch
+        self.key_valid = key_valid_vector(mask)
 
     def causal_view(self):
         """The causal variant (create_causal_attention_mask) sharing this key-validity vector."""

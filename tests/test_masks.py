@@ -117,3 +117,83 @@ def test_gpu_none_mask_raises():
     m = S.SelfAttention(64, 4).cuda()
     with pytest.raises(TypeError):
         m(torch.randn(2, 8, 64, device="cuda"), None)
+
+
+# ---- the key-validity predicate (model/utils.py:8-12, 19-23): keep a key only where the fp32
+# mask value is exactly 1 — 1.0 - mask is masked wherever it is non-zero ----
+ODD_VALUES = [1.0, 2.0, 0.5, 0.0, -1.0, 1.0, 3.0, 1.0]
+
+
+def test_key_valid_predicate_matches_the_reference_masks():
+    """The traced / host form of the predicate against the oracle's restatement of
+    create_attention_mask: a key is kept exactly where the additive mask is 0."""
+    from scattennet_amd.ops import key_valid_vector
+    for dtype in (torch.float32, torch.float64, torch.int64, torch.int32, torch.float16, torch.bfloat16):
+        m = torch.tensor([ODD_VALUES, ODD_VALUES[::-1]]).to(dtype)
+        kv = key_valid_vector(m)
+        want = (O.additive_key_mask(m)[:, 0, 0] == 0).float()
+        assert torch.equal(kv, want), dtype
+    nan = torch.tensor([[1.0, float("nan"), 1.0]])
+    assert torch.equal(key_valid_vector(nan), torch.tensor([[1.0, 0.0, 1.0]]))
+    assert torch.equal(key_valid_vector(torch.tensor([[True, False]])), torch.tensor([[1.0, 0.0]]))
+
+
+@pytest.mark.gpu
+def test_gpu_key_valid_kernel_every_dtype():
+    """sca_key_valid (one launch, no ATen) against the reference predicate for every mask dtype."""
+    from scattennet_amd.ops import key_valid_vector
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    g = torch.Generator().manual_seed(3)
+    vals = torch.tensor([1.0, 2.0, 0.5, 0.0, -1.0, 3.0, 1.0 + 2 ** -20])
+    m = vals[torch.randint(0, len(vals), (5, 301), generator=g)]
+    m[:, ::3] = 1.0
+    for dtype in (torch.float32, torch.float64, torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8,
+                  torch.bool, torch.float16, torch.bfloat16):
+        md = m.to(dtype)
+        want = (O.additive_key_mask(md)[:, 0, 0] == 0).float()
+        got = key_valid_vector(md.cuda())
+        assert torch.equal(got.cpu(), want), dtype
+    assert key_valid_vector(torch.empty(0, 4, dtype=torch.long, device="cuda")).shape == (0, 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.int64, torch.float32])
+def test_gpu_sca_stack_with_non_binary_mask_vs_oracle(dtype):
+    """The SCA stack fed a (B, T) mask holding 2, 0.5, -1 besides 0 / 1: keys are kept only
+    where the mask is 1, as the reference's mask builders decide (model/utils.py:3-28)."""
+    import scattennet_amd as S
+    from scattennet_amd import workloads as W
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    torch.manual_seed(5)
+    B, T, d, H = 3, 40, 64, 4
+    cfg = W.model_cfg(d, H, 2, maxpos=T)
+    sca = S.SeparativeCoordinateAttention(cfg).eval()
+    vals = torch.tensor([1.0, 1.0, 1.0, 2.0, 0.5, 0.0, -1.0])
+    mask = vals[torch.randint(0, len(vals), (B, T))]
+    mask[0, :5] = 1.0
+    mask[1] = 2.0  # every key of clip 1 masked: uniform attention, as in the reference
+    if dtype == torch.int64:
+        mask = mask.round().to(torch.int64)  # 0.5 -> 0 (masked), 2 / -1 kept as such
+    x, y = torch.randn(B, T, d), torch.randn(B, T, d)
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in sca.state_dict().items()}
+    sca = sca.to(dev)
+    xg, yg = x.to(dev).requires_grad_(True), y.to(dev).requires_grad_(True)
+    out = sca(xg, yg, mask.to(dev))
+    gout = torch.randn(out.shape)
+    out.backward(gout.to(dev))
+    xr, yr = x.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    ref = O.sca({"s." + k: v for k, v in p.items()}, "s", xr, yr, mask, cfg)
+    assert rel_err(out, ref) < PARITY_TOL
+    (ref * gout).sum().backward()
+    assert rel_err(xg.grad, xr.grad) < PARITY_TOL and rel_err(yg.grad, yr.grad) < PARITY_TOL
+    gscale = max(float(v.grad.abs().max()) for v in p.values() if v.grad is not None)
+    named = dict(sca.named_parameters())
+    for k, v in p.items():
+        if v.grad is not None:
+            assert close(named[k].grad.cpu(), v.grad, PARITY_TOL, gscale), (k, rel_err(named[k].grad.cpu(), v.grad))
+    # and the result differs from treating every non-zero as "keep" (the old predicate)
+    ref_nz = O.sca({"s." + k: v.detach() for k, v in p.items()}, "s", x, y, (mask != 0).long(), cfg)
+    assert rel_err(ref_nz, ref.detach()) > 1e-2
