@@ -47,7 +47,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from scattennet_amd import ops, workloads as W  # noqa: E402
-from scattennet_amd.dp import GradBuckets  # noqa: E402
+from scattennet_amd.dp import GradBuckets, gathered_mean  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA == fp32 vector peak
 HBM_PEAK_GBS = 8000.0
@@ -229,6 +229,11 @@ def main(args):
     clips = w["B"] * world * args.steps / elapsed
     step_flops = W.flops_per_step(w)
 
+    # ---- data parallel: the averaged buckets checked once against an eager gather-and-mean ----
+    dp_check = None
+    if reducer is not None and reducer.collective and args.dropout == 0:
+        dp_check = check_allreduce(reducer, graph, fwd_bwd, sync, params)
+
     # ---- dominant-kernel roofline: one instrumented eager step (HIP events per launch) ----
     prof = ops.LaunchProfiler()
     with prof:
@@ -284,10 +289,46 @@ def main(args):
                 "backend": dist.get_backend(), "buckets_mb": [round(b / 2 ** 20, 2) for b in reducer.bucket_sizes()],
                 "overlapped": reducer.overlap, "in_graph": reducer.overlap and graph is not None,
                 "fallback_params": len(reducer.last_fallback)}
+            if dp_check is not None:
+                line["config"]["grad_allreduce"].update(dp_check)
         print(json.dumps(line), flush=True)
     if use_dp:
         reducer.close()
         dist.destroy_process_group()
+
+
+def check_allreduce(reducer, graph, fwd_bwd, sync, params):
+    """Once, after the timed region: the averaged gradient buckets of one step (a graph replay,
+    or an eager step) against an eager all_gather of every rank's LOCAL gradients of the same
+    step, summed in rank order and divided by the world size (dp.gathered_mean).  The local
+    gradients come from the same step run with the reducer's collectives off (the kernels are
+    deterministic, so they are the gradients the replay fed its all-reduces)."""
+    if graph is not None:
+        graph.replay()
+    else:
+        for p in params:
+            p.grad = None
+        fwd_bwd()
+    sync()
+    torch.cuda.synchronize()
+    averaged = reducer.flat.clone()
+    reducer.collective = False
+    try:
+        for p in params:
+            p.grad = None
+        fwd_bwd()
+        torch.cuda.synchronize()
+        local = reducer.flat.clone()
+    finally:
+        reducer.collective = True
+    ref = gathered_mean(local)
+    diff = float((averaged - ref).abs().max())
+    scale = float(ref.abs().max())
+    spread = float((local - ref).abs().max())  # how far this rank's own gradients are from the mean
+    return {"check_max_abs": diff, "check_rel": diff / scale if scale > 0 else 0.0,
+            "check_local_vs_mean_max_abs": spread,
+            "check": "captured AVG buckets vs eager all_gather + mean of the ranks' local gradients, one step "
+                     "after the timed region"}
 
 
 def _kstats_name(raw):

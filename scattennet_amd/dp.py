@@ -65,6 +65,7 @@ class GradBuckets:
         self.bucket_bytes = int(float(bucket_mb if bucket_mb is not None else
                                       os.environ.get("SCA_DP_BUCKET_MB", "25")) * 2 ** 20)
         backend = dist.get_backend() if dist.is_initialized() else None
+        self.backend = backend  # "nccl" (RCCL): AVG all-reduces; any other: pre-scale + SUM
         if overlap is None:
             overlap = backend == "nccl" and os.environ.get("SCA_DP_OVERLAP", "1") != "0"
         self.overlap = bool(overlap)
@@ -233,8 +234,12 @@ class GradBuckets:
             self._step["works"].append(dist.all_reduce(bucket, async_op=True))
             return
 
+        avg = self.average and self.backend == "nccl"  # gloo has no AVG: pre-scale, then SUM
+
         def body():  # synchronous form: enqueued on the communication stream
-            dist.all_reduce(bucket, op=dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM)
+            if self.average and not avg:
+                bucket.mul_(1.0 / self.world)
+            dist.all_reduce(bucket, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM)
 
         if events is None:
             comm = self._on_comm(self._step["streams"][b].values(), body)
@@ -370,3 +375,19 @@ class GradAllReduce(GradBuckets):
 
     def __call__(self):
         self.sync()
+
+
+def gathered_mean(local):
+    """Mean over ranks of every rank's `local` tensor, summed in rank order after an eager
+    all_gather (outside any capture): the reference value for the averaged buckets of a
+    data-parallel step (bench.py prints max |buckets - this| at world size > 1).  Over gloo
+    the gather runs on host copies."""
+    world = dist.get_world_size()
+    on_host = dist.get_backend() != "nccl"
+    src = local.detach().cpu() if on_host else local.detach().contiguous()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src)
+    acc = parts[0].clone()
+    for t in parts[1:]:
+        acc.add_(t)
+    return acc.div_(world).to(local.device)

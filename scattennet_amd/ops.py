@@ -547,7 +547,7 @@ def _ln_bwd_or_handoff(dys, vs, gam, means, rstds, lnsaved, bet):
 
     def reduce():
         reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
-    finish = (reduce, part, params, (pairs, nblk, N))
+    finish = (reduce, part, params, (pairs, nblk, N), list(dg) + list(db))
     if not _LN_AFFINE_SIDE:
         reduce()
         params_produced(params)
@@ -591,7 +591,8 @@ def _ln_bwd(dys, x, gam, means, rstds, defer_affine=False, params=None):
     finish = None
     if defer_affine:  # pointers only: see _ln_bwd_or_handoff
         pairs = _ptr_pairs([(part[g], dg[g]) for g in range(G)] + [(part[g], db[g], nblk * N) for g in range(G)])
-        finish = (lambda: reduce_rows_ptr(pairs, nblk, 1, N, N, 0), part, params or (), (pairs, nblk, N))
+        finish = (lambda: reduce_rows_ptr(pairs, nblk, 1, N, N, 0), part, params or (), (pairs, nblk, N),
+                  list(dg) + list(db))
     else:
         params_produced(params or ())
     return dx, dg, db, finish
@@ -886,27 +887,75 @@ _affine_task = None  # the autograd graph task the pending entries belong to
 
 
 _flush_queued = [None]  # the autograd graph task whose final callbacks hold a flush
+_side_written = {}  # id(parameter) -> graph task whose side stream wrote its gradient
 _AFFINE_DEFER_MAX = 256 * 512  # partial-row floats per problem up to which a LayerNormAdd defers
 
 
-def _affine_deferrable(params):
+def _plain_leaf(p):
+    """A parameter whose gradient autograd hands over untouched until the backward ends: a leaf
+    that requires grad, holds no .grad to add to and has no hooks (a tensor hook or a
+    post-accumulate-grad hook would read the gradient as soon as it is returned — before a
+    side-stream or deferred launch has written it)."""
+    return (p.is_leaf and p.requires_grad and p.grad is None and not p._backward_hooks and
+            getattr(p, "_post_accumulate_grad_hooks", None) is None)
+
+
+def _affine_deferrable(params, needed=None):
     """Whether a LayerNorm's dgamma / dbeta reduction may be deferred to the end of the backward:
     autograd takes the (not yet written) gradient tensors over as .grad, which is safe only
-    for leaf parameters without a .grad to add to."""
-    return _AFFINE_DEFER and not _LIBRARY_MODE and all(p.is_leaf and p.grad is None for p in params)
+    for plain leaf parameters (_plain_leaf) whose gradients the backward asked for."""
+    return (_AFFINE_DEFER and not _LIBRARY_MODE and all(_plain_leaf(p) for p in params) and
+            (needed is None or all(needed)))
+
+
+def _keep(ts):
+    """Storage references that keep gradient buffers allocated until a deferred launch has been
+    enqueued, without raising the tensors' use count (autograd's AccumulateGrad copies a
+    gradient tensor that anything else references instead of taking it over)."""
+    return [t.untyped_storage() for t in ts if t is not None]
+
+
+def _mark_unsettled(params):
+    """Record that this backward returned these parameters' gradients before writing them (side
+    stream or deferred reduction)."""
+    task = torch._C._current_graph_task_id()
+    if len(_side_written) > 4096:
+        _side_written.clear()
+    for p in params:
+        _side_written[id(p)] = task
+
+
+def _settle_reuse(params):
+    """A parameter used twice in one backward whose first gradient is still pending (written on
+    the side stream, or left to a deferred reduction): autograd adds the new gradient into the
+    first one on the current stream, so the pending work is launched and joined here first.
+    True when that happened (the caller then computes on the current stream)."""
+    task = torch._C._current_graph_task_id()
+    if not any(_side_written.get(id(p)) == task for p in params):
+        return False
+    flush_deferred_affine()
+    main = torch.cuda.current_stream()
+    for streams, _ in _side_streams.values():
+        for st in streams:
+            main.wait_stream(st)
+            note_join(main, st)
+    return True
 
 
 def _affine_finish(part, dg, db, nblk, N, params, defer):
     """dgamma / dbeta = fixed-order sums of the per-block partial rows: now, or (defer) collected
     on the current stream and launched with the other deferred reductions by
-    flush_deferred_affine, which a final backward callback runs at the latest."""
+    flush_deferred_affine, which a final backward callback runs at the latest (the entry keeps
+    the partials and the dgamma / dbeta buffers allocated until then: autograd may drop the
+    gradients it did not ask for)."""
     G = len(part)
     pairs = _ptr_pairs([(part[g], dg[g]) for g in range(G)] + [(part[g], db[g], nblk * N) for g in range(G)])
     if not defer:
         reduce_rows_ptr(pairs, nblk, 1, N, N, 0)
         params_produced(params)
         return
-    _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(part), list(params)))
+    _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(part) + _keep(list(dg) + list(db)),
+                                                list(params)))
     task = torch._C._current_graph_task_id()  # one flush callback per backward (a backward that
     if _flush_queued[0] != task:               # raised before its callbacks leaves no stale flag)
         _flush_queued[0] = task
@@ -926,9 +975,13 @@ def _affine_defer(st, entry):
 
 def flush_deferred_affine():
     """Launch every collected affine reduction on the side stream it was deferred on, grouped
-    by (blocks, width), and report its parameters as produced."""
+    by (blocks, width), and report its parameters as produced.  Entries of another backward
+    (one that raised before its final callbacks: its gradients are void) are dropped."""
     _flush_queued[0] = None
     if not _affine_pending:
+        return
+    if _affine_task != torch._C._current_graph_task_id():
+        _affine_pending.clear()
         return
     pend = list(_affine_pending.values())
     _affine_pending.clear()
@@ -958,7 +1011,8 @@ def weight_grads(items, M=None, extra=None, ready=None):
         if extra is not None:
             if defer and len(extra) > 3:
                 pairs, nblk, N = extra[3]
-                _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(extra[1]), list(extra[2])))
+                _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(extra[1]) + _keep(extra[4]),
+                                                            list(extra[2])))
             else:
                 extra[0]()
                 params_produced(extra[2])
@@ -968,12 +1022,14 @@ def weight_grads(items, M=None, extra=None, ready=None):
     # as this returns (ordered on the current stream only), and so does a non-leaf parameter
     # view (precision.fp32_compute's p.float(): its cast backward reads the gradient at once):
     # compute on the current stream
-    params = [it[3] for it in items] + list(extra[2] if extra is not None else ())
-    if not _WGRAD_SIDE or _LIBRARY_MODE or any(not p.is_leaf or p.grad is not None for p in params):
+    params = [it[3] for it in items] + [it[4] for it in items if torch.is_tensor(it[4])] + \
+        list(extra[2] if extra is not None else ())
+    if _settle_reuse(params) or not _WGRAD_SIDE or _LIBRARY_MODE or not all(_plain_leaf(p) for p in params):
         return run()
     dev = items[0][0].device
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
+    _mark_unsettled(params)
     if ready is not None:
         side.wait_event(ready)  # dY and X were ready at this point of the main stream
     else:
@@ -983,6 +1039,8 @@ def weight_grads(items, M=None, extra=None, ready=None):
         it[0].record_stream(side)
         it[1].record_stream(side)
     for t in (extra[1] if extra is not None else ()):
+        t.record_stream(side)
+    for t in (extra[4] if extra is not None else ()):  # dgamma / dbeta, written on the side stream
         t.record_stream(side)
     with torch.cuda.stream(side):
         out = run(defer=_AFFINE_DEFER)
@@ -1259,8 +1317,9 @@ def _softmax_rows_launch(pairs, rows, N, bwd=False):
 
 
 def _attn_fwd_gemm(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop):
-    if drop:
-        raise ValueError("attention dropout with head size > 128 is not supported")
+    """drop: None or (p, seeds): o = dropout(P) v with the kernels' mask (sca_dropout over the
+    (B, H, Tq, Tk) probabilities, element ((b H + h) Tq + i) Tk + j, attention.py:67-69); P
+    itself (undropped) is kept for the backward."""
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
@@ -1281,7 +1340,11 @@ def _attn_fwd_gemm(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop):
                 soft.append((S.data_ptr(), None, S.data_ptr()))
     gemm(L.GEMM_NT, probs)
     _softmax_rows_launch(soft, Tq, Tk)
-    probs = [_raw_prob(P[g][b, h].data_ptr(), v[g].data_ptr() + 4 * (b * Tk * d + h * hd), Tk, d, Tk,
+    Pv = P
+    if drop:
+        Pv = [torch.empty_like(t) for t in P]
+        dropout_apply([(P[g], Pv[g], drop[1][g]) for g in range(G)], drop[0])
+    probs = [_raw_prob(Pv[g][b, h].data_ptr(), v[g].data_ptr() + 4 * (b * Tk * d + h * hd), Tk, d, Tk,
                        o[g].data_ptr() + 4 * (b * Tq * d + h * hd), Tq, hd, d)
              for g in range(G) for b in range(B) for h in range(H)]
     gemm(L.GEMM_NN, probs)
@@ -1289,7 +1352,9 @@ def _attn_fwd_gemm(G, H, causal, plus_one, key_valid, add_mask, q, k, v, drop):
     return o, [p.view(-1) for p in P], [q[0].new_empty(0) for _ in range(G)]
 
 
-def _attn_bwd_gemm(G, H, q, k, v, P, dout, dq_scale, dv_scale):
+def _attn_bwd_gemm(G, H, q, k, v, P, dout, dq_scale, dv_scale, drop=None):
+    """With dropout (p, seeds): dP = dropout(dO v^T) (the same mask and 1/(1-p): the gradient of
+    dropout(P)), dv = dropout(P)^T dO."""
     B, Tq, d = q[0].shape
     Tk = k[0].shape[1]
     hd = d // H
@@ -1303,10 +1368,15 @@ def _attn_bwd_gemm(G, H, q, k, v, P, dout, dq_scale, dv_scale):
     # dP = dO v^T  (into dS), then dS = softmax_bwd(P, dP) in place
     gemm(L.GEMM_NT, [_raw_prob(dout[g].data_ptr() + off(b, h, Tq), v[g].data_ptr() + off(b, h, Tk), d, d, hd,
                                dS[g][b, h].data_ptr(), Tq, Tk, Tk) for g, b, h in idx])
+    Pv = P
+    if drop:
+        dropout_apply([(dS[g], dS[g], drop[1][g]) for g in range(G)], drop[0])
+        Pv = [torch.empty_like(t) for t in P]
+        dropout_apply([(P[g], Pv[g], drop[1][g]) for g in range(G)], drop[0])
     _softmax_rows_launch([(P[g][b, h].data_ptr(), dS[g][b, h].data_ptr(), dS[g][b, h].data_ptr())
                           for g, b, h in idx], Tq, Tk, bwd=True)
     # dv = P^T dO, dk = dS^T q (TN over the Tq rows); dq = dS k (NN)
-    gemm(L.GEMM_TN, [_raw_prob(P[g][b, h].data_ptr(), dout[g].data_ptr() + off(b, h, Tq), Tk, d, Tq,
+    gemm(L.GEMM_TN, [_raw_prob(Pv[g][b, h].data_ptr(), dout[g].data_ptr() + off(b, h, Tq), Tk, d, Tq,
                                dv[g].data_ptr() + off(b, h, Tk), Tk, hd, d, alpha=dv_scale) for g, b, h in idx])
     gemm(L.GEMM_TN, [_raw_prob(dS[g][b, h].data_ptr(), q[g].data_ptr() + off(b, h, Tq), Tk, d, Tq,
                                dk[g].data_ptr() + off(b, h, Tk), Tk, hd, d) for g, b, h in idx])
@@ -1352,7 +1422,7 @@ def _attn_bwd(G, H, causal, plus_one, key_valid, add_mask, q, k, v, o, sm, sl, d
     Tk = k[0].shape[1]
     hd = d // H
     if hd > _KERNEL_HD[-1]:  # the GEMM path: sm is P
-        return _attn_bwd_gemm(G, H, q, k, v, sm, dout, dq_scale, dv_scale)
+        return _attn_bwd_gemm(G, H, q, k, v, sm, dout, dq_scale, dv_scale, drop)
     hdp = _padded_hd(hd)
     if hdp != hd:
         qp, kp, vp, op, dop = (_pad_heads(ts, H, hd, hdp) for ts in (q, k, v, o, dout))
@@ -1784,7 +1854,10 @@ class LayerNormAdd(Function):
         # deferred when the partial rows are few (config 2 / 3: +0.5-0.7 %); config 5's 1024 x 512
         # partials per problem reduce better beside the weight gradients where they fall (-0.4 %
         # deferred; profiles/r05_misc/affine_defer2_ab.txt)
-        defer = _affine_deferrable(params) and L.lib().sca_layernorm_bwd_blocks(rows) * N <= _AFFINE_DEFER_MAX
+        defer = (not _settle_reuse(params) and _affine_deferrable(params, ctx.needs_input_grad[-2 * G:]) and
+                 L.lib().sca_layernorm_bwd_blocks(rows) * N <= _AFFINE_DEFER_MAX)
+        if defer:
+            _mark_unsettled(params)
         if hs is not None:  # dL/dv (= dL/dx) done; the dgamma / dbeta partials summed below
             dx, part, nblk = [h[2] for h in hs], [h[3] for h in hs], hs[0][4]
         else:

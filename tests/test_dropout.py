@@ -273,6 +273,9 @@ def test_graph_replays_draw_fresh_masks():
     ("causal", 2, 270, 270, 64, 2, False),
     ("self", 2, 70, 70, 128, 2, False),     # hd 64: split dq / dkdv kernels
     ("cross", 2, 40, 50, 64, 4, True),      # a materialised additive mask: the general path
+    ("self", 2, 40, 40, 320, 2, False),     # hd 160 > 128: GEMM + row-softmax path, sca_dropout on P
+    ("causal", 2, 36, 36, 256, 1, False),   # hd 256
+    ("cross", 2, 30, 44, 320, 2, True),
 ])
 def test_attention_probability_dropout(kind, B, Tq, Tk, d, H, explicit, seedlog):
     """attention.py:67-69 / 119-121 / 173-175: F.dropout on the softmax probabilities in

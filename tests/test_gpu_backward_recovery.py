@@ -47,3 +47,155 @@ def test_backward_after_a_raised_backward():
     assert set(got) == set(ref)
     for n, g in got.items():
         assert torch.equal(g, ref[n]), n
+
+
+def _grads(model):
+    return {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
+def _setup(seed=3):
+    dev = torch.device("cuda:0")
+    w = dict(W.WORKLOADS["cfg2"], B=2)
+    model = W.build_streams(w, dev, seed=seed, init="random")
+    kp, mask, gout = W.synthetic_batch(w, dev, seed=5, ragged=True)
+    return model, kp, mask, gout
+
+
+def test_stale_reductions_are_dropped_when_the_next_backward_defers_nothing():
+    """After a raised backward, a flush outside that backward (or from a backward that defers
+    nothing, e.g. accumulating into held .grad) launches none of its pending reductions."""
+    from scattennet_amd import ops
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    model, kp, mask, gout = _setup()
+
+    def run(x):
+        outs = model(x, mask)
+        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+
+    run(kp)
+    torch.cuda.synchronize()
+    ref = _grads(model)
+    kp_bad = kp.clone().requires_grad_(True)
+    kp_bad.register_hook(lambda _: (_ for _ in ()).throw(RuntimeError("boom")))
+    model.zero_grad(set_to_none=True)
+    with pytest.raises(RuntimeError, match="boom"):
+        run(kp_bad)
+    torch.cuda.synchronize()
+    for n, p in model.named_parameters():  # the void gradients of the raised backward, held on
+        if p.grad is not None:             # purpose: a stale reduction would write into them
+            p.grad = ref[n].clone()
+    held = _grads(model)
+    ops.flush_deferred_affine()  # outside any backward: must drop, not launch
+    assert not ops._affine_pending
+    torch.cuda.synchronize()
+    for n, g in _grads(model).items():
+        assert torch.equal(g, held[n]), n
+    run(kp)  # accumulates into the held gradients: nothing deferred
+    torch.cuda.synchronize()
+    for n, g in _grads(model).items():
+        assert torch.equal(g, held[n] + ref[n]), n
+
+
+def _reference_grads(model, run):
+    """The same backward with every gradient written in place on the calling stream (no side
+    stream, no deferred reductions)."""
+    from scattennet_amd import ops
+    side, defer = ops._WGRAD_SIDE, ops._AFFINE_DEFER
+    ops._WGRAD_SIDE, ops._AFFINE_DEFER = False, False
+    try:
+        model.zero_grad(set_to_none=True)
+        out = run()
+        torch.cuda.synchronize()
+        return _grads(model), out
+    finally:
+        ops._WGRAD_SIDE, ops._AFFINE_DEFER = side, defer
+        model.zero_grad(set_to_none=True)
+
+
+def _churn(dev):
+    """Allocations that would take over any gradient block freed too early."""
+    return [torch.full((1 << 16,), 7.0, device=dev) for _ in range(64)]
+
+
+def test_frozen_layernorm_gradients_match_the_in_place_path():
+    """A frozen LayerNorm (requires_grad False: autograd drops its dgamma / dbeta) must not
+    leave a deferred reduction writing into freed memory; every other gradient bitwise equal to
+    the in-place path."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    model, kp, mask, gout = _setup()
+    frozen = [m for n, m in model.named_modules() if n.endswith("attn_layer_norm")][:3]
+    for m in frozen:
+        m.weight.requires_grad_(False)
+        m.bias.requires_grad_(False)
+
+    def run():
+        outs = model(kp, mask)
+        keep = _churn(kp.device)
+        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+        return keep
+
+    ref, _ = _reference_grads(model, run)
+    keep = run()
+    torch.cuda.synchronize()
+    got = _grads(model)
+    assert set(got) == set(ref)
+    for n, g in got.items():
+        assert torch.equal(g, ref[n]), n
+    for t in keep:
+        assert bool((t == 7.0).all())
+    for m in frozen:
+        assert m.weight.grad is None and m.bias.grad is None
+
+
+def test_input_only_autograd_grad_leaves_parameters_alone():
+    """torch.autograd.grad w.r.t. the keypoints only: no parameter gradient is kept, the input
+    gradient equals the in-place path's, and no live tensor is overwritten."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    model, kp, mask, gout = _setup()
+    x = kp.clone().requires_grad_(True)
+
+    def run():
+        outs = model(x, mask)
+        keep = _churn(kp.device)
+        (g,) = torch.autograd.grad(outs, [x], [gout[i] for i in range(len(outs))])
+        return g, keep
+
+    _, (ref, _) = _reference_grads(model, run)
+    got, keep = run()
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert all(p.grad is None for p in model.parameters())
+    for t in keep:
+        assert bool((t == 7.0).all())
+
+
+def test_a_block_used_twice_accumulates_complete_gradients():
+    """The same attention block applied twice in one graph: autograd adds the second weight
+    gradient into the first on the calling stream, so the first (side stream) must be complete
+    by then."""
+    import scattennet_amd as S
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    torch.manual_seed(11)
+    cfg = W.model_cfg(256, 16, 1, maxpos=64)
+    blk = S.CoordinateAttention(cfg, "self_attn").to(dev)
+    x = torch.randn(4, 64, 256, device=dev)
+    mask = S.key_padding_mask(torch.ones(4, 64, dtype=torch.long, device=dev))
+    g = torch.randn(4, 64, 256, device=dev)
+
+    def run():
+        y = blk(blk(x, mask), mask)
+        y.backward(g)
+
+    ref, _ = _reference_grads(blk, run)
+    blk.zero_grad(set_to_none=True)
+    run()
+    torch.cuda.synchronize()
+    got = _grads(blk)
+    assert set(got) == set(ref)
+    for n, t in got.items():
+        assert torch.allclose(t, ref[n], rtol=0, atol=1e-6 * float(ref[n].abs().max())), n

@@ -228,3 +228,75 @@ def _cfg4_shards(monkeypatch):
     rscale = max(float(v.abs().max()) for v in grads.values())
     for k, v in grads.items():
         assert close(shard_sum[k].cpu(), v, PARITY_TOL, rscale), (k, rel_err(shard_sum[k].cpu(), v))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", ["nccl", "gloo"])
+def test_bucketed_reducer_averages_two_ranks(monkeypatch, backend):
+    """The overlapped reducer's averaging at world size 2, driven through the RCCL branch of
+    dp.GradBuckets._launch with a stand-in second rank: every bucket all-reduce issued by the
+    reducer receives the other rank's bucket (its local gradients of a different batch, at
+    the same offsets) — AVG: (mine + other) / 2; with the gloo backend (no AVG) the reducer
+    must pre-scale by 1/2 and ask for SUM.  The result must be the mean of the two ranks'
+    local gradients, bucket by bucket, bitwise."""
+    import torch.distributed as dist
+
+    from scattennet_amd import ops, workloads as W
+    from scattennet_amd.dp import GradBuckets
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda:0")
+    w = dict(W.WORKLOADS["cfg2"], B=2, T=64)
+    model = W.build_streams(w, dev, seed=6, init="random")
+    kp_a, mask_a, gout_a = W.synthetic_batch(w, dev, seed=31, ragged=True)
+    kp_b, mask_b, gout_b = W.synthetic_batch(w, dev, seed=32, ragged=True)
+    init_here = not dist.is_initialized()
+    if init_here:
+        port = 29900 + os.getpid() % 90
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    red = GradBuckets(model.parameters(), world=2, bucket_mb=4, overlap=True)
+    red.backend = backend
+    params = list(model.parameters())
+
+    def step(kp, mask, gout):
+        for p in params:
+            p.grad = None
+        outs = model(kp, mask)
+        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+        red.sync()
+        torch.cuda.synchronize()
+        return red.flat.clone()
+
+    try:
+        red.collective = False
+        step(kp_a, mask_a, gout_a)  # discovery step (builds the plan)
+        local_a = step(kp_a, mask_a, gout_a)
+        local_b = step(kp_b, mask_b, gout_b)
+        red.collective = True
+        ops_seen = []
+        real = dist.all_reduce
+
+        def second_rank(t, op=dist.ReduceOp.SUM, **k):
+            o = (t.data_ptr() - red.flat.data_ptr()) // 4
+            other = local_b[o:o + t.numel()]
+            ops_seen.append((op, o, t.numel()))
+            if op == dist.ReduceOp.AVG:
+                t.add_(other).mul_(0.5)
+            else:  # the other rank pre-scaled its bucket as this one did
+                t.add_(other * 0.5)
+            return real(t, op=dist.ReduceOp.SUM, **k)  # world 1: identity
+
+        monkeypatch.setattr(dist, "all_reduce", second_rank)
+        got = step(kp_a, mask_a, gout_a)
+        want_op = dist.ReduceOp.AVG if backend == "nccl" else dist.ReduceOp.SUM
+        assert len(ops_seen) == len(red.plan) and all(op == want_op for op, _, _ in ops_seen), ops_seen
+        assert sorted(o for _, o, _ in ops_seen) == [o for o, _, _ in red.plan]
+        want = (local_a + local_b) * 0.5 if backend == "nccl" else local_a * 0.5 + local_b * 0.5
+        for o, n, _ in red.plan:
+            assert torch.equal(got[o:o + n], want[o:o + n]), o
+        assert not torch.equal(local_a, local_b)
+    finally:
+        red.close()
+        ops.set_grad_sink(None)
+        if init_here:
+            dist.destroy_process_group()
