@@ -1854,7 +1854,7 @@ class LayerNormAdd(Function):
         # deferred when the partial rows are few (config 2 / 3: +0.5-0.7 %); config 5's 1024 x 512
         # partials per problem reduce better beside the weight gradients where they fall (-0.4 %
         # deferred; profiles/r05_misc/affine_defer2_ab.txt)
-        defer = (not _settle_reuse(params) and _affine_deferrable(params, ctx.needs_input_grad[-2 * G:]) and
+        defer = (not _settle_reuse(params) and _affine_deferrable(params, (getattr(ctx, "needs_input_grad", None) or (True,))[-2 * G:]) and
                  L.lib().sca_layernorm_bwd_blocks(rows) * N <= _AFFINE_DEFER_MAX)
         if defer:
             _mark_unsettled(params)
