@@ -3,7 +3,7 @@ stream; MODE "one": after chain kernel F a side stream forks and runs S matmuls;
 after every chain kernel i >= F a side kernel forks (event recorded before chain kernel i+1 is
 captured: the side kernel is child 1, as the weight gradients of ops.weight_grads), all side
 kernels on one side stream; joined at the end.  Run under rocprofv3 --kernel-trace and read the
-start times (tools/_call.sh prints the last replay).
+start times (the last replay is printed).
 
     python tools/graph_fork_probe.py MODE N F S
 """

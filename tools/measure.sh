@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-5 measurement set (each step under its own time limit; the first failure stops the call):
-#   bash tools/r05_measure.sh tests <set>  -> full GPU suite, smoke, the bench lines (cfg2 with the
+# Measurement set (each step under its own time limit; the first failure stops the call):
+#   bash tools/measure.sh tests <set>  -> full GPU suite, smoke, the bench lines (cfg2 with the
 #                                            CPU baseline, cfg3, cfg5, cfg2 with dropout 0.2)
-#   bash tools/r05_measure.sh prof <set>   -> per workload (WLS, default cfg2 cfg3 cfg5): rocprofv3
+#   bash tools/measure.sh prof <set>   -> per workload (WLS, default cfg2 cfg3 cfg5): rocprofv3
 #                                            kernel trace + stats, PMC traffic, SQ utilisation
 # Results under gpurun_out/<set>/; then, here: python tools/promote_profile.py <wl>
 #   gpurun_out/<set>/prof_<wl> gpurun_out/<set>/pmc_<wl> gpurun_out/<set>/sq_<wl>
 set -o pipefail
-set_=${2:-r05}
+set_=${2:-m}
 out=gpurun_out/$set_
 mkdir -p $out
 if [ "$1" = tests ]; then

@@ -1,5 +1,5 @@
 """Per-kernel MFMA busy, wave-state shares and effective clock from one rocprofv3 run with
---kernel-trace and --pmc (SQ counters + GRBM_GUI_ACTIVE) — tools/r05_tn_pmc.sh.
+--kernel-trace and --pmc (SQ counters + GRBM_GUI_ACTIVE) — tools/tn_pmc.sh.
 
     python tools/tn_pmc2.py <dir>
 """
