@@ -38,6 +38,11 @@ struct GemmArgs {
   long bias_off[SCA_GEMM_MAX_PROBLEMS];         // split-K: problem's first bias partial row in ws
   unsigned* counters;                           // split-K combined in-launch (sca_gemm_splitk_fused)
   int nprob;                                    // problems in p[]
+  // flat grid (gemm_tnk_kernel): workgroups of problem i are tile_beg[i] .. tile_beg[i + 1] - 1,
+  // its own tiles x splits only — problems of different shapes share a launch without the
+  // empty workgroups of a max-shape grid
+  int flat;
+  int tile_beg[SCA_GEMM_MAX_PROBLEMS + 1];
 };
 
 // Workgroup tile configuration.
@@ -778,11 +783,28 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
   const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   const unsigned xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bx = wgid % gx, by = (wgid / gx) % gy, bz = wgid / (gx * gy);
-
   const int splitk = args.splitk;
-  const int pid = bz / splitk;
-  const int ks = bz % splitk;
+  int bx, by, pid, ks;
+  long cnt_idx;  // the tile's split-K counter
+  if (args.flat) {
+    int p = 0;
+    while (p + 1 < args.nprob && (int)wgid >= args.tile_beg[p + 1]) ++p;
+    const int tn = (args.p[p].N + GL_BN - 1) / GL_BN, tm = (args.p[p].M + GL_BM - 1) / GL_BM;
+    int local = (int)wgid - args.tile_beg[p];
+    bx = local % tn;
+    local /= tn;
+    by = local % tm;
+    ks = local / tm;
+    pid = p;
+    cnt_idx = args.tile_beg[p] / splitk + (long)by * tn + bx;
+  } else {
+    bx = wgid % gx;
+    by = (wgid / gx) % gy;
+    const int bz = wgid / (gx * gy);
+    pid = bz / splitk;
+    ks = bz % splitk;
+    cnt_idx = (long)pid * gx * gy + (long)by * gx + bx;
+  }
   const sca_gemm_problem& P = args.p[pid];
   const int m0 = by * GL_BM, n0 = bx * GL_BN;
   if (m0 >= P.M || n0 >= P.N) return;
@@ -1031,7 +1053,7 @@ __global__ __launch_bounds__(256) void gemm_tnk_kernel(const GemmArgs args) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     unsigned* flag = reinterpret_cast<unsigned*>(smem);  // the partial tiles are consumed
-    unsigned* cnt = args.counters + (long)pid * gx * gy + (long)by * gx + bx;
+    unsigned* cnt = args.counters + cnt_idx;
     if (threadIdx.x == 0)
       *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(splitk - 1);
     __syncthreads();
@@ -2562,8 +2584,20 @@ bool vec_ok(const GemmArgs& a, int nprob, int layout) {
 }
 
 template <int S, int SUB, bool REG = false>
-int launch_tnk(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+int launch_tnk(GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
   dim3 grid((maxN + GL_BN - 1) / GL_BN, (maxM + GL_BM - 1) / GL_BM, nprob * a.splitk);
+  bool same = true;
+  for (int i = 1; i < nprob; ++i) same = same && a.p[i].M == a.p[0].M && a.p[i].N == a.p[0].N;
+  if (!same) {  // problems of different shapes: a flat grid of every problem's own tiles x splits
+    a.flat = 1;
+    int t = 0;
+    for (int i = 0; i < nprob; ++i) {
+      a.tile_beg[i] = t;
+      t += ((a.p[i].M + GL_BM - 1) / GL_BM) * ((a.p[i].N + GL_BN - 1) / GL_BN) * a.splitk;
+    }
+    a.tile_beg[nprob] = t;
+    grid = dim3(t, 1, 1);
+  }
   hipLaunchKernelGGL((gemm_tnk_kernel<S, SUB, REG>), grid, dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
@@ -2728,6 +2762,7 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   a.ws = workspace;
   a.drop_off = sca_drop_offset_ptr();
   a.counters = nullptr;
+  a.flat = 0;
   int maxM = 0, maxN = 0;
   for (int i = 0; i < nprob; ++i) {
     const sca_gemm_problem& P = probs[i];

@@ -250,6 +250,7 @@ class GradBuckets:
     def _finish(self):
         # this callback runs before the side streams' join callbacks: the deferred LayerNorm
         # affine reductions report their parameters now
+        ops.flush_held()
         ops.flush_deferred_affine()
         self._launch_ready()  # the last bucket(s)
         st, self._step = self._step, None

@@ -633,6 +633,7 @@ _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per
 _TNK_TILES_PER_PROBLEM = 48
 _TNR = os.environ.get("SCA_TNR", "1") != "0"  # A/B switch for variant 46
 _TNR_SK = int(os.environ.get("SCA_TNR_SK", "0"))  # A/B: one split-K for every variant-46 launch
+_TNR_MIXED = os.environ.get("SCA_TNR_MIXED", "1") != "0"  # A/B: variant-46 launches of mixed shapes
 
 
 # the 128x128 register-staged weight-gradient kernel with interleaved phases (tile 43) for long
@@ -852,6 +853,8 @@ def _queue_join(main, side):
 
     def _join():
         _join_pending[key] = None
+        if _held["entries"]:
+            _flush_held(main, side)
         flush_deferred_affine()
         main.wait_stream(side)
         note_join(main, side)
@@ -933,6 +936,7 @@ def _settle_reuse(params):
     task = torch._C._current_graph_task_id()
     if not any(_side_written.get(id(p)) == task for p in params):
         return False
+    flush_held()
     flush_deferred_affine()
     main = torch.cuda.current_stream()
     for streams, _ in _side_streams.values():
@@ -1008,14 +1012,7 @@ def weight_grads(items, M=None, extra=None, ready=None):
     def run(defer=False):
         out = _weight_grads(items)
         params_produced([p for it in items for p in (it[3], it[4])])
-        if extra is not None:
-            if defer and len(extra) > 3:
-                pairs, nblk, N = extra[3]
-                _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(extra[1]) + _keep(extra[4]),
-                                                            list(extra[2])))
-            else:
-                extra[0]()
-                params_produced(extra[2])
+        _run_extra(extra, defer)
         return out
 
     # a parameter that already holds a .grad gets the new gradient added by autograd as soon
@@ -1030,51 +1027,185 @@ def weight_grads(items, M=None, extra=None, ready=None):
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
     _mark_unsettled(params)
+    if _WGRAD_HOLD_FRAC > 0:
+        task = torch._C._current_graph_task_id()
+        if _held["task"] != task:  # (held sections of a backward that raised are void)
+            if _held["task"] is not None and _held["count"] > 0:
+                _held["last_total"] = _held["count"]
+            _held.update(task=task, n=0, count=0, entries=[], hold=_hold_count())
+        _held["count"] += 1
+        hold = _held["hold"]
+        if _held["n"] < hold:
+            # held: the gradients are allocated and returned now, their launches issued together
+            # with the following held sections' at the last one's fork (or at the join).  The
+            # entry keeps the operands, raw-pointer problems and the gradients' STORAGES only:
+            # a reference to a returned gradient tensor would make autograd copy it (unwritten)
+            _held["n"] += 1
+            out = _wgrad_alloc(items)
+            ex = None if extra is None else (extra[0], extra[1], extra[2], extra[3] if len(extra) > 3 else None,
+                                             _keep(extra[4]))
+            _held["entries"].append((items, ex, _wgrad_specs(items, out),
+                                     _keep([t for o in out for t in o])))
+            if _held["n"] == hold:
+                _flush_held(main, side, ready)
+            else:
+                _queue_join(main, side)
+            return out
     if ready is not None:
         side.wait_event(ready)  # dY and X were ready at this point of the main stream
     else:
         side.wait_stream(main)  # dY and X are ready on the main stream
     note_fork(side, main, "weight-gradient side stream")
-    for it in items:  # keep their memory from being reused by the main stream too early
-        it[0].record_stream(side)
-        it[1].record_stream(side)
-    for t in (extra[1] if extra is not None else ()):
-        t.record_stream(side)
-    for t in (extra[4] if extra is not None else ()):  # dgamma / dbeta, written on the side stream
-        t.record_stream(side)
+    _record_on(side, items, extra)
     with torch.cuda.stream(side):
         out = run(defer=_AFFINE_DEFER)
     _queue_join(main, side)
     return out
 
 
+def _run_extra(extra, defer):
+    """The LayerNorm affine reduction riding in a weight-gradient section: now, or deferred."""
+    if extra is None:
+        return
+    if defer and len(extra) > 3:
+        pairs, nblk, N = extra[3]
+        _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(extra[1]) + _keep(extra[4]), list(extra[2])))
+    else:
+        extra[0]()
+        params_produced(extra[2])
+
+
+def _record_on(side, items, extra, outs=()):
+    """Keep the section's operands (and gradient buffers written there) from being reused by
+    the main stream before the side stream's launches have run."""
+    for it in items:
+        it[0].record_stream(side)
+        it[1].record_stream(side)
+    for t in (extra[1] if extra is not None else ()):
+        t.record_stream(side)
+    for t in (extra[4] if extra is not None else ()):  # dgamma / dbeta, written on the side stream
+        t.record_stream(side)
+    for dW, db in outs:
+        dW.record_stream(side)
+        if db is not None:
+            db.record_stream(side)
+
+
+# SCA_WGRAD_HOLD=n (A/B): the first n weight-gradient sections of a backward are not forked one
+# by one: their launches are issued together (problems of equal shape across sections in one
+# grouped launch) at the n-th section's fork — one fork marker instead of n, fuller launches
+# SCA_WGRAD_HOLD=n (an integer: n sections) or a fraction f < 1 (the first f of the previous
+# backward's sections; the first backward holds none)
+_WGRAD_HOLD_FRAC = float(os.environ.get("SCA_WGRAD_HOLD", "0"))
+_held = {"task": None, "n": 0, "count": 0, "entries": [], "hold": 0, "last_total": 0}
+
+
+def _hold_count():
+    if _WGRAD_HOLD_FRAC >= 1:
+        return int(_WGRAD_HOLD_FRAC)
+    return int(round(_WGRAD_HOLD_FRAC * _held["last_total"]))
+
+
+def flush_held():
+    """Issue any held weight-gradient sections now (the data-parallel reducer's finish: every
+    gradient must have been produced before it reduces the last buckets)."""
+    if _held["entries"]:
+        dev = _held["entries"][0][0][0][0].device
+        main = torch.cuda.current_stream(dev)
+        _flush_held(main, _side_stream(dev))
+
+
+def _flush_held(main, side, ready=None):
+    """Launch the held weight-gradient sections on the side stream, forked at `ready` (else at
+    the main stream's current point)."""
+    ents = _held["entries"]
+    _held["entries"] = []
+    if not ents or _held["task"] != torch._C._current_graph_task_id():
+        return
+    if ready is not None:
+        side.wait_event(ready)
+    else:
+        side.wait_stream(main)
+    note_fork(side, main, "weight-gradient side stream (held sections)")
+    for items, ex, _, stores in ents:
+        _record_on(side, items, None)
+        for t in (ex[1] if ex is not None else ()):
+            t.record_stream(side)
+        for st in stores + (list(ex[4]) if ex is not None else []):  # gradients written on the side stream
+            torch.empty(0, device=items[0][0].device).set_(st).record_stream(side)
+    with torch.cuda.stream(side):
+        _wgrad_launch([sp for _, _, specs, _ in ents for sp in specs])
+        for items, ex, _, _ in ents:
+            params_produced([p for it in items for p in (it[3], it[4])])
+            if ex is None:
+                continue
+            if _AFFINE_DEFER and ex[3] is not None:
+                pairs, nblk, N = ex[3]
+                _affine_defer(torch.cuda.current_stream(), (pairs, nblk, N, list(ex[1]) + list(ex[4]), list(ex[2])))
+            else:
+                ex[0]()
+                params_produced(ex[2])
+
+
 def _weight_grads(items):
-    """Allocate the gradients and launch the grouped split-K TN GEMMs."""
+    """Allocate the gradients and launch the grouped split-K TN GEMMs -> [(dW, db)]."""
+    out = _wgrad_alloc(items)
+    _wgrad_launch(_wgrad_specs(items, out))
+    return out
+
+
+def _norm_items(items):
+    return [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
+
+
+def _wgrad_alloc(items):
     out = []
-    launches = []
-    by_shape = {}  # problems of one launch: one (out, in, rows) shape
-    items = [it if len(it) == 6 else tuple(it) + (it[2],) for it in items]
-    for idx, (dY, X, alpha, W, bias, _) in enumerate(items):
-        n_out, n_in = W.shape
+    for dY, X, alpha, W, bias, _ in _norm_items(items):
         dW = param_grad_empty(W)
         if torch.is_tensor(bias):
             db = param_grad_empty(bias)
         else:
-            db = torch.empty(n_out, device=W.device, dtype=W.dtype) if bias else None
+            db = torch.empty(W.shape[0], device=W.device, dtype=W.dtype) if bias else None
         out.append((dW, db))
-        key = (n_out, n_in, dY.shape[0])
-        by_shape.setdefault(key, []).append(idx)
-    for idxs in by_shape.values():
-        for c in range(0, len(idxs), L.GEMM_MAX_PROBLEMS):
-            sub = idxs[c:c + L.GEMM_MAX_PROBLEMS]
-            tiles = sum(((items[i][3].shape[0] + 63) // 64) * ((items[i][3].shape[1] + 63) // 64) for i in sub)
-            sk = _splitk_for(items[sub[0]][0].shape[0], tiles)
+    return out
+
+
+def _wgrad_specs(items, out):
+    """One (shape key, problem) per item; the problem holds raw pointers only (no tensor
+    references: a held section must not raise its gradients' use count)."""
+    specs = []
+    for (dY, X, alpha, W, _, bscale), (dW, db) in zip(_norm_items(items), out):
+        n_out, n_in = W.shape
+        Mr = dY.shape[0]
+        specs.append(((n_out, n_in, Mr), _prob([_seg(dY, X, n_out, n_in, Mr, alpha)], dW, n_out, n_in, n_in,
+                                              bias_grad=db, bias_grad_scale=bscale / alpha)))
+    return specs
+
+
+def _wgrad_launch(specs):
+    """Grouped launches of the weight-gradient problems: equal (out, in, rows) shapes share a
+    launch (up to GEMM_MAX_PROBLEMS), the kernel variant and split-K chosen per launch."""
+    if not specs:
+        return
+    by_shape = {}
+    for key, prob in specs:
+        n_out, n_in, Kr = key
+        # the k-split kernel (variant 46) takes problems of different shapes in one flat grid:
+        # they share a launch by reduction length alone (an FFN's fc1 and fc2 weight gradients)
+        mixed = _TNR_MIXED and _TNR and Kr % 64 == 0 and Kr >= 128 and not (0 < _TNB_MIN_K <= Kr)
+        by_shape.setdefault((0, 0, Kr) if mixed else key, []).append((key, prob))
+    launches = []
+    for (_, _, Kr), allkp in by_shape.items():
+        for c in range(0, len(allkp), L.GEMM_MAX_PROBLEMS):
+            subk = allkp[c:c + L.GEMM_MAX_PROBLEMS]
+            sub = [pr for _, pr in subk]
+            n_out, n_in = max(k[0] for k, _ in subk), max(k[1] for k, _ in subk)
+            tiles = sum(((k[0] + 63) // 64) * ((k[1] + 63) // 64) for k, _ in subk)
+            sk = _splitk_for(Kr, tiles)
             tile = 0
-            Kr = items[sub[0]][0].shape[0]
             if 0 < _TNB_MIN_K <= Kr and Kr % 64 == 0:
                 tile = 43
-                sk = _tnb_split(Kr, sum(-(-items[i][3].shape[0] // 128) * -(-items[i][3].shape[1] // 128)
-                                        for i in sub))
+                sk = _tnb_split(Kr, len(sub) * -(-n_out // 128) * -(-n_in // 128))
             elif _TNR and Kr % 64 == 0 and Kr >= 128:
                 # the k-split kernel with the register-staged, interleaved operand stream (variant
                 # 46): 6-20 % faster than both the LDS-DMA k-split (36) and the plain LDS-DMA
@@ -1084,7 +1215,7 @@ def _weight_grads(items):
                 # problems are FFN-sized (config 2's 4 x (768, 256): +0.6 % in step over 2); the
                 # many small problems of config 3's attention (12 x (256, 256)) run better at 2
                 # in step (+1.1 %, profiles/r05_misc/tnr_split_rule_ab.txt) though 4 is faster alone
-                big = all(items[i][3].shape[0] * items[i][3].shape[1] >= 768 * 256 for i in sub)
+                big = all(k[0] * k[1] >= 768 * 256 for k, _ in subk)
                 tile, sk = 46, (4 if tiles * 4 == 768 and Kr >= 2048 and big else (2 if Kr >= 512 else 1))
                 if _TNR_SK and Kr // _TNR_SK >= 256:
                     sk = _TNR_SK
@@ -1095,19 +1226,12 @@ def _weight_grads(items):
                 # the 64x64 LDS-DMA kernel at split 3; the FFN launches at split 2 instead of 4
                 # write half the partial slabs, same step time; profiles/r04_probe/ab_tnk_ffn.txt)
                 tile, sk = 36, min(sk, 2)
-            probs, wsz = [], 0
-            for i in sub:
-                dY, X, alpha, W, _, bscale = items[i]
-                n_out, n_in = W.shape
-                Mr = dY.shape[0]
-                probs.append(_prob([_seg(dY, X, n_out, n_in, Mr, alpha)], out[i][0], n_out, n_in, n_in,
-                                   bias_grad=out[i][1], bias_grad_scale=bscale / alpha))
-                wsz += sk * (n_out * n_in + n_out)
-            ws = torch.empty(wsz, device=items[0][0].device, dtype=torch.float32) if sk > 1 else None
-            launches.append((probs, sk, ws, tile))
+            wsz = sum(sk * (k[0] * k[1] + k[0]) for k, _ in subk)
+            ws = torch.empty(wsz, device=torch.device("cuda", torch.cuda.current_device()),
+                             dtype=torch.float32) if sk > 1 else None
+            launches.append((sub, sk, ws, tile))
     for p, k, w, tl in launches:
         gemm(L.GEMM_TN, p, splitk=k, ws=w, tile=tl)
-    return out
 
 
 def sum_tensors(groups):

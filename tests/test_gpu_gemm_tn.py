@@ -126,3 +126,19 @@ def test_ksplit_is_deterministic(tile):
         outs.append([(dW.clone(), db.clone()) for _, _, dW, db in items])
     for (a, b), (c, d) in zip(*outs):
         assert torch.equal(a, c) and torch.equal(b, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("splitk", [1, 2, 4])
+def test_mixed_shape_launch_flat_grid(splitk):
+    """One variant-46 launch holding problems of different shapes (an FFN's fc1 and fc2 weight
+    gradients, 768 x 256 and 256 x 768, and a few odd ones): the flat grid of each problem's
+    own tiles x splits, with the in-launch split-K combine, against float64."""
+    from scattennet_amd import _lib as L, ops
+    shapes = [(192, 64), (64, 192)] * 6 + [(100, 68), (68, 100), (256, 256), (40, 36)]
+    items = _case(shapes, 512, seed=40 + splitk)
+    probs = _probs(items, alpha=0.5, bscale=2.0)
+    ws = torch.empty(sum(splitk * (p.M * p.N + p.M) for p in probs), device="cuda") if splitk > 1 else None
+    ops.gemm(L.GEMM_TN, probs, splitk=splitk, ws=ws, tile=46)
+    torch.cuda.synchronize()
+    _check(items, alpha=0.5, bscale=2.0)

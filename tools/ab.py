@@ -17,6 +17,7 @@ on stdout (mean / min / max clips/s per variant, and the ratio to the first vari
 import argparse
 import json
 import os
+import shlex
 import statistics
 import subprocess
 import sys
@@ -78,7 +79,7 @@ def main():
         if args.pre:
             log = os.path.join(out, f"pre_{v['name']}.log")
             cmd = ["timeout", "-k", "10", str(args.timeout), sys.executable, "-u", "-m", "pytest", "-x", "-q",
-                   "-p", "no:cacheprovider", "--timeout", "240", "--timeout-method", "thread"] + args.pre.split()
+                   "-p", "no:cacheprovider", "--timeout", "240", "--timeout-method", "thread"] + shlex.split(args.pre)
             with open(log, "w") as f:
                 rc = subprocess.run(cmd, cwd=ROOT, env=v["full_env"], stdout=f, stderr=subprocess.STDOUT).returncode
             print(f"[{v['name']}] pre: rc={rc} {open(log).read().strip().splitlines()[-1:]}", flush=True)
