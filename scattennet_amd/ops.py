@@ -633,7 +633,8 @@ _SPLITK_SLOTS = 768  # workgroup slots per round: 3 LDS-DMA 64x64 workgroups per
 _TNK_TILES_PER_PROBLEM = 48
 _TNR = os.environ.get("SCA_TNR", "1") != "0"  # A/B switch for variant 46
 _TNR_SK = int(os.environ.get("SCA_TNR_SK", "0"))  # A/B: one split-K for every variant-46 launch
-_TNR_MIXED = os.environ.get("SCA_TNR_MIXED", "1") != "0"  # A/B: variant-46 launches of mixed shapes
+_TNR_MIXED = os.environ.get("SCA_TNR_MIXED", "0") != "0"  # A/B: mixed-shape variant-46 launches (-0.7 % in step)
+_TNR_MIXED_SK = int(os.environ.get("SCA_TNR_MIXED_SK", "0"))  # A/B: split-K of mixed-shape launches
 
 
 # the 128x128 register-staged weight-gradient kernel with interleaved phases (tile 43) for long
@@ -1001,7 +1002,7 @@ def flush_deferred_affine():
                 params_produced(params)
 
 
-def weight_grads(items, M=None, extra=None, ready=None):
+def weight_grads(items, M=None, extra=None, ready=None, holdable=False):
     """dW_g = alpha_g * dY_g^T X_g  (TN layout, split-K) and db_g = bias_scale_g * colsum(dY_g),
     the bias gradient fused into the same GEMM (its first column tile sums the dY slices).
 
@@ -1032,7 +1033,10 @@ def weight_grads(items, M=None, extra=None, ready=None):
         if _held["task"] != task:  # (held sections of a backward that raised are void)
             if _held["task"] is not None and _held["count"] > 0:
                 _held["last_total"] = _held["count"]
-            _held.update(task=task, n=0, count=0, entries=[], hold=_hold_count())
+            # only a backward that begins with the SCA blocks' sections holds (config 2); one that
+            # begins elsewhere (config 3: fusion, residual network) forks every section
+            _held.update(task=task, n=0, count=0, entries=[], hold=_hold_count() if holdable else 0)
+    if _WGRAD_HOLD_FRAC > 0 and holdable:
         _held["count"] += 1
         hold = _held["hold"]
         if _held["n"] < hold:
@@ -1048,8 +1052,7 @@ def weight_grads(items, M=None, extra=None, ready=None):
                                      _keep([t for o in out for t in o])))
             if _held["n"] == hold:
                 _flush_held(main, side, ready)
-            else:
-                _queue_join(main, side)
+            _queue_join(main, side)
             return out
     if ready is not None:
         side.wait_event(ready)  # dY and X were ready at this point of the main stream
@@ -1096,7 +1099,9 @@ def _record_on(side, items, extra, outs=()):
 # grouped launch) at the n-th section's fork — one fork marker instead of n, fuller launches
 # SCA_WGRAD_HOLD=n (an integer: n sections) or a fraction f < 1 (the first f of the previous
 # backward's sections; the first backward holds none)
-_WGRAD_HOLD_FRAC = float(os.environ.get("SCA_WGRAD_HOLD", "0"))
+_WGRAD_HOLD_FRAC = float(os.environ.get("SCA_WGRAD_HOLD", "0.45"))
+_WGRAD_HOLD_MERGE = os.environ.get("SCA_WGRAD_HOLD_MERGE", "1") != "0"
+
 _held = {"task": None, "n": 0, "count": 0, "entries": [], "hold": 0, "last_total": 0}
 
 
@@ -1134,7 +1139,11 @@ def _flush_held(main, side, ready=None):
         for st in stores + (list(ex[4]) if ex is not None else []):  # gradients written on the side stream
             torch.empty(0, device=items[0][0].device).set_(st).record_stream(side)
     with torch.cuda.stream(side):
-        _wgrad_launch([sp for _, _, specs, _ in ents for sp in specs])
+        if _WGRAD_HOLD_MERGE:  # equal shapes across the held sections share launches
+            _wgrad_launch([sp for _, _, specs, _ in ents for sp in specs])
+        else:  # each section's own launches, issued back to back
+            for _, _, specs, _ in ents:
+                _wgrad_launch(specs)
         for items, ex, _, _ in ents:
             params_produced([p for it in items for p in (it[3], it[4])])
             if ex is None:
@@ -1217,6 +1226,8 @@ def _wgrad_launch(specs):
                 # in step (+1.1 %, profiles/r05_misc/tnr_split_rule_ab.txt) though 4 is faster alone
                 big = all(k[0] * k[1] >= 768 * 256 for k, _ in subk)
                 tile, sk = 46, (4 if tiles * 4 == 768 and Kr >= 2048 and big else (2 if Kr >= 512 else 1))
+                if _TNR_MIXED_SK and len({k for k, _ in subk}) > 1 and Kr // _TNR_MIXED_SK >= 256:
+                    sk = _TNR_MIXED_SK
                 if _TNR_SK and Kr // _TNR_SK >= 256:
                     sk = _TNR_SK
             elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
@@ -1733,7 +1744,7 @@ class AttentionBlock(Function):
             items += [(_flat(dq[g]), xf, 1.0, Wq, bq), (_flat(dk[g]), kf, 1.0, Wk, bk),
                       (_flat(dv[g]), kf, 1.0, Wv, bv, 1.0 / av),
                       (_flat(dyo[g]), _flat(o[g]), 1.0, Wo[g], bo[g])]
-        wg = weight_grads(items, extra=ln_finish, ready=ready)
+        wg = weight_grads(items, extra=ln_finish, ready=ready, holdable=True)
         dW, dWo, dbo = [], [], []
         for g in range(G):
             for j in range(3):
@@ -1890,7 +1901,7 @@ class FeedForwardResidual(Function):
         items = [(_flat(dyo[g]), acts[g], 1.0, W2[g], ctx.b2[g] if ctx.b2[g] is not None else True)
                  for g in range(G)] + \
                 [(dz[g], _flat(x[g]), 1.0, W1[g], ctx.b1[g] if ctx.b1[g] is not None else True) for g in range(G)]
-        wg = weight_grads(items, extra=ln_finish, ready=ready)
+        wg = weight_grads(items, extra=ln_finish, ready=ready, holdable=True)
         dW2 = [wg[g] for g in range(G)]
         dW1 = [wg[G + g] for g in range(G)]
         return (None,) * 5 + tuple(dx) + tuple(w for w, _ in dW1) + tuple(b for _, b in dW1) + \

@@ -201,3 +201,31 @@ def test_a_block_used_twice_accumulates_complete_gradients():
     assert set(got) == set(ref)
     for n, t in got.items():
         assert torch.allclose(t, ref[n], rtol=0, atol=1e-6 * float(ref[n].abs().max())), n
+
+
+@pytest.mark.parametrize("hold", [1, 5, 10, 19, 40])
+def test_held_weight_gradient_sections_match_the_in_place_path(hold, monkeypatch):
+    """ops.weight_grads holding the first `hold` SCA sections of a backward and issuing them
+    together (equal shapes across sections in shared launches) at the last one's fork — or at
+    the join when the backward has fewer sections: every gradient bitwise equal to the in-place
+    path's (same kernels, same reduction order per problem)."""
+    from scattennet_amd import ops
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    model, kp, mask, gout = _setup(seed=7)
+    monkeypatch.setattr(ops, "_WGRAD_HOLD_FRAC", float(hold))
+
+    def run():
+        outs = model(kp, mask)
+        torch.autograd.backward(outs, [gout[g] for g in range(len(outs))])
+
+    ref, _ = _reference_grads(model, run)
+    for _ in range(2):  # the second backward holds by the first's section count too
+        model.zero_grad(set_to_none=True)
+        run()
+        torch.cuda.synchronize()
+        got = _grads(model)
+        assert set(got) == set(ref)
+        for n, g in got.items():
+            assert torch.equal(g, ref[n]), n
+    assert not ops._held["entries"]
