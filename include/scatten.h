@@ -233,6 +233,12 @@ int sca_gemm_tile_override(int layout, int tile);
 int sca_gemm_variant(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                      unsigned* counters, int variant, void* stream);
 
+/* The kernel a sca_gemm_variant launch of these problems would run (variant 0: the override or
+ * the heuristic), as a short name ("gemm_tnk_kernel<3, 1, true>", ...) written into buf
+ * (NUL-terminated, truncated to len).  Host-only: no GPU call; for profiling records.      */
+int sca_gemm_kernel_name(int layout, int nprob, const sca_gemm_problem* probs, int splitk, int variant, char* buf,
+                         int len);
+
 /* Fused masked attention over (B, T, H*hd) row-major activations (head h at columns
  * h*hd .. h*hd+hd-1, row stride ld*).  Scores use q as given (the projection already
  * applied hd^-0.5).  Masking, per query row i and key j:

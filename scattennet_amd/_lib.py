@@ -129,6 +129,7 @@ EXPORTS = {
     "sca_gemm_splitk_counters": ([c_int, c_int, c_int], c_long),
     "sca_gemm_splitk_fused": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     "sca_gemm_variant": ([c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p], c_int),
+    "sca_gemm_kernel_name": ([c_int, c_int, c_void_p, c_int, c_int, ctypes.c_char_p, c_int], c_int),
     "sca_gemm_ln": ([c_int, c_void_p, c_void_p, c_float, c_void_p], c_int),
     "sca_gemm_ln_rows": ([c_int, c_int, c_int], c_int),
     "sca_gemm_ln_force_rows": ([c_int], c_int),

@@ -2654,44 +2654,91 @@ int launch_tnb(const GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st)
   return hipGetLastError() == hipSuccess ? SCA_OK : SCA_ERR_LAUNCH;
 }
 
-template <int LAYOUT>
-int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
-  if (!vec_ok(a, nprob, LAYOUT)) return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
+// The kernel a launch of `tile` (a requested variant) runs after the eligibility fallbacks —
+// launch_tile dispatches on it and sca_gemm_kernel_name reports it (profiling names).
+enum KernelId {
+  K_T1_ANY, K_NTB45, K_NTB44, K_NTB41, K_NTB42, K_TNK46, K_TNB43, K_TNB38, K_TNB39, K_TNB40, K_TNK36, K_TNK37,
+  K_GLDS3, K_GLDS2, K_GLDS4, K_T5, K_T7, K_T1
+};
+
+KernelId resolve_kernel(int layout, int tile, const GemmArgs& a, int nprob) {
+  if (!vec_ok(a, nprob, layout)) return K_T1_ANY;
   if (tile == 41 || tile == 42 || tile == 44 || tile == 45) {
-    constexpr bool KN = LAYOUT == SCA_GEMM_NN;
-    if (LAYOUT != SCA_GEMM_TN && ntb_ok(a, nprob, KN)) {
-      if (tile == 45) return launch_ntb<true, 6, KN, true, 64>(a, nprob, maxM, maxN, st);
-      if (tile == 44) return launch_ntb<true, 6, KN, true>(a, nprob, maxM, maxN, st);
-      return tile == 41 ? launch_ntb<true, 6, KN>(a, nprob, maxM, maxN, st)
-                        : launch_ntb<false, 2, KN>(a, nprob, maxM, maxN, st);
-    }
-    tile = LAYOUT == SCA_GEMM_NT ? 20 : 21;
+    if (layout != SCA_GEMM_TN && ntb_ok(a, nprob, layout == SCA_GEMM_NN))
+      return tile == 45 ? K_NTB45 : tile == 44 ? K_NTB44 : tile == 41 ? K_NTB41 : K_NTB42;
+    tile = layout == SCA_GEMM_NT ? 20 : 21;
   }
   if (tile == 46) {
-    if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) return launch_tnk<3, 1, true>(a, nprob, maxM, maxN, st);
+    if (layout == SCA_GEMM_TN && tnb_ok(a, nprob)) return K_TNK46;
     tile = 36;
   }
   if ((tile >= 38 && tile <= 40) || tile == 43) {
-    if (LAYOUT == SCA_GEMM_TN && tnb_ok(a, nprob)) {
-      if (tile == 43) return launch_tnb<true, 6, true>(a, nprob, maxM, maxN, st);
-      if (tile == 38) return launch_tnb<false, 2>(a, nprob, maxM, maxN, st);
-      return tile == 39 ? launch_tnb<true, 4>(a, nprob, maxM, maxN, st) : launch_tnb<true, 6>(a, nprob, maxM, maxN, st);
-    }
+    if (layout == SCA_GEMM_TN && tnb_ok(a, nprob))
+      return tile == 43 ? K_TNB43 : tile == 38 ? K_TNB38 : tile == 39 ? K_TNB39 : K_TNB40;
     tile = 36;
   }
   if (tile >= kTnFirst && tile <= kTnLast) {
-    if (LAYOUT == SCA_GEMM_TN && tn_ok(a, nprob))
-      return tile == 36 ? launch_tnk<3, 1>(a, nprob, maxM, maxN, st) : launch_tnk<4, 1>(a, nprob, maxM, maxN, st);
+    if (layout == SCA_GEMM_TN && tn_ok(a, nprob)) return tile == 36 ? K_TNK36 : K_TNK37;
     tile = 21;
   }
-  if (tile >= 20 && !glds_ok(a, nprob)) tile = LAYOUT == SCA_GEMM_TN ? 5 : (LAYOUT == SCA_GEMM_NN ? 7 : 1);
+  if (tile >= 20 && !glds_ok(a, nprob)) tile = layout == SCA_GEMM_TN ? 5 : (layout == SCA_GEMM_NN ? 7 : 1);
   switch (tile) {
-    case 20: return launch_glds<LAYOUT, 3>(a, nprob, maxM, maxN, st);
-    case 21: return launch_glds<LAYOUT, 2>(a, nprob, maxM, maxN, st);
-    case 22: return launch_glds<LAYOUT, 4>(a, nprob, maxM, maxN, st);
-    case 5: return launch<LAYOUT, T5>(a, nprob, maxM, maxN, st);
-    case 7: return launch<LAYOUT, T7>(a, nprob, maxM, maxN, st);
+    case 20: return K_GLDS3;
+    case 21: return K_GLDS2;
+    case 22: return K_GLDS4;
+    case 5: return K_T5;
+    case 7: return K_T7;
+    default: return K_T1;
+  }
+}
+
+template <int LAYOUT>
+int launch_tile(int tile, GemmArgs& a, int nprob, int maxM, int maxN, hipStream_t st) {
+  constexpr bool KN = LAYOUT == SCA_GEMM_NN;
+  switch (resolve_kernel(LAYOUT, tile, a, nprob)) {
+    case K_T1_ANY: return launch<LAYOUT, T1, false>(a, nprob, maxM, maxN, st);
+    case K_NTB45: return launch_ntb<true, 6, KN, true, 64>(a, nprob, maxM, maxN, st);
+    case K_NTB44: return launch_ntb<true, 6, KN, true>(a, nprob, maxM, maxN, st);
+    case K_NTB41: return launch_ntb<true, 6, KN>(a, nprob, maxM, maxN, st);
+    case K_NTB42: return launch_ntb<false, 2, KN>(a, nprob, maxM, maxN, st);
+    case K_TNK46: return launch_tnk<3, 1, true>(a, nprob, maxM, maxN, st);
+    case K_TNB43: return launch_tnb<true, 6, true>(a, nprob, maxM, maxN, st);
+    case K_TNB38: return launch_tnb<false, 2>(a, nprob, maxM, maxN, st);
+    case K_TNB39: return launch_tnb<true, 4>(a, nprob, maxM, maxN, st);
+    case K_TNB40: return launch_tnb<true, 6>(a, nprob, maxM, maxN, st);
+    case K_TNK36: return launch_tnk<3, 1>(a, nprob, maxM, maxN, st);
+    case K_TNK37: return launch_tnk<4, 1>(a, nprob, maxM, maxN, st);
+    case K_GLDS3: return launch_glds<LAYOUT, 3>(a, nprob, maxM, maxN, st);
+    case K_GLDS2: return launch_glds<LAYOUT, 2>(a, nprob, maxM, maxN, st);
+    case K_GLDS4: return launch_glds<LAYOUT, 4>(a, nprob, maxM, maxN, st);
+    case K_T5: return launch<LAYOUT, T5>(a, nprob, maxM, maxN, st);
+    case K_T7: return launch<LAYOUT, T7>(a, nprob, maxM, maxN, st);
     default: return launch<LAYOUT, T1>(a, nprob, maxM, maxN, st);
+  }
+}
+
+// rocprofv3-style short names of the resolved kernels (layout substituted where templated)
+int kernel_name(int layout, KernelId k, char* buf, int len) {
+  const char* kn = layout == SCA_GEMM_NN ? "true" : "false";
+  switch (k) {
+    case K_T1_ANY: return snprintf(buf, len, "gemm_kernel<%d, T1, false>", layout);
+    case K_NTB45: return snprintf(buf, len, "gemm_ntb_kernel<true, 6, %s, true, 64>", kn);
+    case K_NTB44: return snprintf(buf, len, "gemm_ntb_kernel<true, 6, %s, true, 128>", kn);
+    case K_NTB41: return snprintf(buf, len, "gemm_ntb_kernel<true, 6, %s, false, 128>", kn);
+    case K_NTB42: return snprintf(buf, len, "gemm_ntb_kernel<false, 2, %s, false, 128>", kn);
+    case K_TNK46: return snprintf(buf, len, "gemm_tnk_kernel<3, 1, true>");
+    case K_TNB43: return snprintf(buf, len, "gemm_tnb_kernel<true, 6, true>");
+    case K_TNB38: return snprintf(buf, len, "gemm_tnb_kernel<false, 2, false>");
+    case K_TNB39: return snprintf(buf, len, "gemm_tnb_kernel<true, 4, false>");
+    case K_TNB40: return snprintf(buf, len, "gemm_tnb_kernel<true, 6, false>");
+    case K_TNK36: return snprintf(buf, len, "gemm_tnk_kernel<3, 1, false>");
+    case K_TNK37: return snprintf(buf, len, "gemm_tnk_kernel<4, 1, false>");
+    case K_GLDS3: return snprintf(buf, len, "gemm_glds_kernel<%d, 3>", layout);
+    case K_GLDS2: return snprintf(buf, len, "gemm_glds_kernel<%d, 2>", layout);
+    case K_GLDS4: return snprintf(buf, len, "gemm_glds_kernel<%d, 4>", layout);
+    case K_T5: return snprintf(buf, len, "gemm_kernel<%d, T5>", layout);
+    case K_T7: return snprintf(buf, len, "gemm_kernel<%d, T7>", layout);
+    default: return snprintf(buf, len, "gemm_kernel<%d, T1>", layout);
   }
 }
 
@@ -2748,6 +2795,32 @@ extern "C" int sca_gemm_tile_override(int layout, int tile) {
 extern "C" void sca_set_error(const char* msg);
 
 namespace {
+// the requested variant of a launch: the caller's, the process-wide override, or the heuristic
+int choose_tile(int layout, const sca_gemm_problem* probs, int nprob, int splitk, int variant) {
+  long tiles64 = 0;
+  for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
+  int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
+  if (!variant && !g_tile_override[layout] && layout != SCA_GEMM_TN && splitk == 1 && tiles64 >= 2048 &&
+      ntb_default()) {
+    // big forward / input-gradient GEMMs (config 5: 8192-row operands, hundreds of 128x128
+    // tiles): the register-staged 128x128 kernel when every problem's reduction is long
+    // enough (tools/gemm_bench.py --cfg5); launch_tile hands ineligible shapes back to the
+    // LDS-DMA kernel
+    bool longk = true;
+    for (int i = 0; i < nprob; ++i) {
+      int k = 0;
+      for (int s2 = 0; s2 < probs[i].nseg; ++s2) k += probs[i].seg[s2].K;
+      longk = longk && k >= ntb_min_k();
+    }
+    if (longk) tile = 44;
+  }
+  if (!variant && !g_tile_override[layout] && layout != SCA_GEMM_TN && splitk == 1 && tile != 44 &&
+      ntb_default())
+    tile = 45;  // every other NT / NN GEMM: the 64x64 form (tools/gemm_bench.py: +5 to +13 % over the
+                // LDS-DMA kernels at config 2's shapes); launch_tile hands ineligible shapes back
+  return tile;
+}
+
 // do_main: the GEMM launch; do_reduce: the split-K slab reduction (splitk > 1 only)
 int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace, void* stream,
               bool do_main, bool do_reduce, unsigned* counters = nullptr, int variant = 0) {
@@ -2814,27 +2887,7 @@ int gemm_impl(int layout, int nprob, const sca_gemm_problem* probs, int splitk, 
   if (maxM == 0 || maxN == 0) return SCA_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int rc;
-  long tiles64 = 0;
-  for (int i = 0; i < nprob; ++i) tiles64 += (long)((probs[i].M + 63) / 64) * ((probs[i].N + 63) / 64);
-  int tile = variant ? variant : pick_tile(layout, tiles64, splitk);
-  if (!variant && !g_tile_override[layout] && layout != SCA_GEMM_TN && splitk == 1 && tiles64 >= 2048 &&
-      ntb_default()) {
-    // big forward / input-gradient GEMMs (config 5: 8192-row operands, hundreds of 128x128
-    // tiles): the register-staged 128x128 kernel when every problem's reduction is long
-    // enough (tools/gemm_bench.py --cfg5); launch_tile hands ineligible shapes back to the
-    // LDS-DMA kernel
-    bool longk = true;
-    for (int i = 0; i < nprob; ++i) {
-      int k = 0;
-      for (int s2 = 0; s2 < probs[i].nseg; ++s2) k += probs[i].seg[s2].K;
-      longk = longk && k >= ntb_min_k();
-    }
-    if (longk) tile = 44;
-  }
-  if (!variant && !g_tile_override[layout] && layout != SCA_GEMM_TN && splitk == 1 && tile != 44 &&
-      ntb_default())
-    tile = 45;  // every other NT / NN GEMM: the 64x64 form (tools/gemm_bench.py: +5 to +13 % over the
-                // LDS-DMA kernels at config 2's shapes); launch_tile hands ineligible shapes back
+  int tile = choose_tile(layout, probs, nprob, splitk, variant);
   // in-launch split-K combine: the 4-wave LDS-DMA kernel only (else the separate reduce runs)
   const bool tn_big =
       layout == SCA_GEMM_TN && ((tile >= kTnFirst && tile <= kTnLast) || tile == 43 || tile == 46) && tn_ok(a, nprob);
@@ -2882,6 +2935,21 @@ extern "C" int sca_gemm_partial(int layout, int nprob, const sca_gemm_problem* p
 extern "C" int sca_gemm_reduce(int layout, int nprob, const sca_gemm_problem* probs, int splitk, float* workspace,
                                void* stream) {
   return gemm_impl(layout, nprob, probs, splitk, workspace, stream, false, true);
+}
+
+extern "C" int sca_gemm_kernel_name(int layout, int nprob, const sca_gemm_problem* probs, int splitk, int variant,
+                                    char* buf, int len) {
+  if (nprob < 1 || nprob > SCA_GEMM_MAX_PROBLEMS || layout < 0 || layout > 2 || splitk < 1 || !buf || len < 1 ||
+      (variant && !valid_tile(layout, variant))) {
+    sca_set_error("sca_gemm_kernel_name: bad arguments");
+    return SCA_ERR_ARG;
+  }
+  GemmArgs a;
+  a.splitk = splitk;
+  a.nprob = nprob;
+  for (int i = 0; i < nprob; ++i) a.p[i] = probs[i];
+  kernel_name(layout, resolve_kernel(layout, choose_tile(layout, probs, nprob, splitk, variant), a, nprob), buf, len);
+  return SCA_OK;
 }
 
 extern "C" long sca_gemm_splitk_counters(int nprob, int maxM, int maxN) {

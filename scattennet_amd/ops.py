@@ -199,53 +199,17 @@ def _splitk_counters(n, device=None):
     return ring[pos:pos + n]
 
 
-_TILE_NAMES = {36: "gemm_tnk_kernel<3, 1, false>", 37: "gemm_tnk_kernel<4, 1, false>"}
 
 
 def _gemm_kernel_name(layout, chunk, tile, splitk=1):
     """The kernel a sca_gemm / sca_gemm_variant launch of `chunk` runs (for the profiler's
-    records): the eligibility rules of gemm.hip's launch_tile (vec_ok, glds_ok, tn_ok) applied
-    to the requested variant (0 = the heuristic: 3-stage LDS-DMA for NT, 2-stage otherwise)."""
-    t = tile or (20 if layout == L.GEMM_NT else 21)
-    if not tile and layout != L.GEMM_TN and splitk == 1 and os.environ.get("SCA_NTB", "1") != "0" and \
-            sum(-(-p.M // 64) * -(-p.N // 64) for p in chunk) >= 2048 and \
-            all(sum(p.seg[j].K for j in range(p.nseg)) >= int(os.environ.get("SCA_NTB_MIN_K", "512"))
-                for p in chunk):
-        t = 44  # gemm.hip gemm_impl: the big NT / NN GEMMs
-    elif not tile and layout != L.GEMM_TN and splitk == 1 and os.environ.get("SCA_NTB", "1") != "0":
-        t = 45  # the 64x64 form for the others
-    a_kc, b_kc = layout != L.GEMM_TN, layout == L.GEMM_NT
-    segs = [(p, p.seg[j]) for p in chunk for j in range(p.nseg)]
-    vec = all(not ((a_kc or b_kc) and g.K % 4) and g.lda % 4 == 0 and g.ldb % 4 == 0 and (g.A or 0) % 16 == 0
-              and (g.B or 0) % 16 == 0 for _, g in segs)
-    if not vec:
-        return f"gemm_kernel<{layout}, T1, false>"
-    glds = all(p.M % 4 == 0 and p.N % 4 == 0 for p in chunk) and \
-        all(g.K % 32 == 0 and g.alpha == p.seg[0].alpha for p, g in segs)
-    if t in (41, 42, 44, 45):
-        if layout != L.GEMM_TN and glds and splitk == 1 and all(p.seg[j].K % 64 == 0 and p.seg[j].K > 0
-                                                                for p in chunk for j in range(p.nseg)):
-            return {41: "gemm_ntb_kernel<true, 6, %s, false, 128>", 42: "gemm_ntb_kernel<false, 2, %s, false, 128>",
-                    44: "gemm_ntb_kernel<true, 6, %s, true, 128>",
-                    45: "gemm_ntb_kernel<true, 6, %s, true, 64>"}[t] % str(layout == L.GEMM_NN).lower()
-        t = 20 if layout == L.GEMM_NT else 21
-    if t == 46:
-        if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
-            return "gemm_tnk_kernel<3, 1, true>"
-        t = 36
-    if t in (38, 39, 40, 43):
-        if layout == L.GEMM_TN and glds and all(p.nseg == 1 and p.seg[0].K % 64 == 0 for p in chunk):
-            return {38: "gemm_tnb_kernel<false, 2, false>", 39: "gemm_tnb_kernel<true, 4, false>",
-                    40: "gemm_tnb_kernel<true, 6, false>", 43: "gemm_tnb_kernel<true, 6, true>"}[t]
-        t = 36
-    if t in _TILE_NAMES:
-        if layout == L.GEMM_TN and glds and all(p.nseg == 1 for p in chunk):
-            return _TILE_NAMES[t]
-        t = 21
-    if t >= 20 and not glds:
-        t = {L.GEMM_TN: 5, L.GEMM_NN: 7}.get(layout, 1)
-    return {20: f"gemm_glds_kernel<{layout}, 3>", 21: f"gemm_glds_kernel<{layout}, 2>",
-            22: f"gemm_glds_kernel<{layout}, 4>"}.get(t, f"gemm_kernel<{layout}, T{t}>")
+    records), as the library's own launcher resolves it (sca_gemm_kernel_name: the variant
+    choice with the process-wide override and the environment switches as the library read
+    them, then the eligibility fallbacks of launch_tile).  Host-only, no GPU call."""
+    buf = ctypes.create_string_buffer(96)
+    arr = (L.GemmProblem * len(chunk))(*chunk)
+    L.check(L.lib().sca_gemm_kernel_name(layout, len(chunk), arr, splitk, tile, buf, 96), "sca_gemm_kernel_name")
+    return buf.value.decode()
 
 
 def gemm(layout, probs, splitk=1, ws=None, tile=0):
