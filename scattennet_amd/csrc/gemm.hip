@@ -2054,6 +2054,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
         int pq = (u >> 2) + prot2;
         pq = pq >= LN.npass ? pq - LN.npass : pq;
         chain_rows(LN.pass[pq], rows, m0, P.M, 32 * wave, lane);
+        if (u == 3) SCA_LN_STAMP(3);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
