@@ -112,3 +112,41 @@ def test_ntb_segments_nt_and_nn(layout_name, tile):
     ref = ref + bias.double().cpu()
     assert _rel(outs[tile].cpu(), ref) < TOL
     assert _rel(outs[tile], outs[20 if layout_name == "NT" else 21]) < TOL
+
+
+@pytest.mark.gpu
+def test_gelu_epilogue_against_exact_erf():
+    """The GEMM epilogues' GELU (branch-free erf, common.h erf_ep) against float64 erf-GELU
+    over pre-activations spanning the whole useful range: max |err| <= 4e-7 * max(1, |z|)
+    (the erf fit's 3.9e-7 plus fp32 rounding), and GELU' (the DGELU epilogue) likewise."""
+    import math
+    from scattennet_amd import _lib as L, ops
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = "cuda"
+    M, N, K = 256, 256, 64
+    z = torch.linspace(-9.0, 9.0, M * N, dtype=torch.float64).reshape(M, N)
+    # z = A B^T with A = z, B = identity blocks: one segment of K = N (an exact product)
+    A = z.float().to(dev)
+    B = torch.eye(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    aux = torch.empty(M, N, device=dev)
+    p = ops._prob([ops._seg(A, B, N, N, N)], C, M, N, N, epi=L.EPI_GELU, aux_out=aux, ldo=N)
+    ops.gemm(L.GEMM_NT, [p])
+    torch.cuda.synchronize()
+    zf = A.double().cpu()
+    want = 0.5 * zf * (1 + torch.special.erf(zf / math.sqrt(2.0)))
+    err = (C.double().cpu() - want).abs() / zf.abs().clamp_min(1.0)
+    assert float(err.max()) <= 4e-7, float(err.max())
+    assert torch.equal(aux.cpu(), A.cpu())  # the pre-activation kept for the backward
+    # DGELU: dY * gelu'(z)
+    dY = torch.ones(M, N, device=dev)
+    D = torch.empty(M, N, device=dev)
+    q = ops._prob([ops._seg(dY, B, N, N, N)], D, M, N, N, epi=L.EPI_DGELU, aux=A, ldx=N)
+    ops.gemm(L.GEMM_NT, [q])
+    torch.cuda.synchronize()
+    cdf = 0.5 * (1 + torch.special.erf(zf / math.sqrt(2.0)))
+    pdf = torch.exp(-0.5 * zf * zf) / math.sqrt(2 * math.pi)
+    gwant = cdf + zf * pdf
+    gerr = (D.double().cpu() - gwant).abs() / zf.abs().clamp_min(1.0)
+    assert float(gerr.max()) <= 1e-6, float(gerr.max())
