@@ -1681,10 +1681,13 @@ __device__ __forceinline__ f32x4 lg_slot(const char* img, int r, int slot) {
 
 // one chained pass's epilogue on float4 row pieces: (acc + bias) * post_scale, GELU (keeps
 // the pre-activation) — epilogue_rows' order
+__device__ __forceinline__ f32x4 chain_bias(const sca_gemm_chain_pass& Q, int nb, int lane) {
+  return Q.bias ? ld4(Q.bias + nb + 4 * (lane & 7)) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 __device__ __forceinline__ void chain_rows(const sca_gemm_chain_pass& Q, const f32x4 (&v)[4], int mb, int M, int nb,
-                                           int lane) {
+                                           int lane, f32x4 bias) {
   const int n = nb + 4 * (lane & 7);
-  const f32x4 bias = Q.bias ? ld4(Q.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = mb + (lane >> 3) + 8 * i;
@@ -2009,8 +2012,14 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       for (int j = 0; j < 2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     lds_barrier();  // the y rows and pass 0's first B tile are in LDS
     SCA_LN_STAMP(2);
+    f32x4 cbias = f32x4{0.f, 0.f, 0.f, 0.f};  // the current pass's bias, loaded at its start
     auto iter2 = [&](auto wr_c, auto ld_c, int u) {
       constexpr bool WR = decltype(wr_c)::value, LDN = decltype(ld_c)::value;
+      if ((u & 3) == 0) {
+        int pq0 = (u >> 2) + prot2;
+        pq0 = pq0 >= LN.npass ? pq0 - LN.npass : pq0;
+        cbias = chain_bias(LN.pass[pq0], 32 * wave, lane);
+      }
       f32x4 a[4][2], b[4][2];
 #pragma unroll
       for (int kc = 0; kc < 4; ++kc)
@@ -2053,7 +2062,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
         for (int q = 0; q < 4; ++q) rows[q] = ld4(scratch + ((lane >> 3) + 8 * q) * EPI_LD + 4 * (lane & 7));
         int pq = (u >> 2) + prot2;
         pq = pq >= LN.npass ? pq - LN.npass : pq;
-        chain_rows(LN.pass[pq], rows, m0, P.M, 32 * wave, lane);
+        chain_rows(LN.pass[pq], rows, m0, P.M, 32 * wave, lane, cbias);
         if (u == 3) SCA_LN_STAMP(3);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -2120,7 +2129,7 @@ __global__ __launch_bounds__(LgCfg<BM>::NW * 64) void gemm_ln_kernel(const GemmL
       if (t == 7) {
         f32x4 rows[4];
         acc_to_rows(acc2, scratch, lane, rows);
-        chain_rows(LN.pass[pass_of(u)], rows, m0, P.M, 32 * wave, lane);
+        chain_rows(LN.pass[pass_of(u)], rows, m0, P.M, 32 * wave, lane, chain_bias(LN.pass[pass_of(u)], 32 * wave, lane));
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
         if (u == 7) SCA_LN_STAMP(3);
