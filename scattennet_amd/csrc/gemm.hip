@@ -2419,9 +2419,19 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   // are younger than slice 0; after a pass's element-form stores (16) the next slice is older
   // than them.  Exact for full tiles; a partial tile waits for everything.
   const bool full = m0 + LB_BM <= P.M;
+  // GELU' operands of a pass (the forward's pre-activations): loaded at the pass's second
+  // slice, behind its third slice's DMA pieces, so their latency is not the pass's tail —
+  // element form (16 per lane) for the passes before the last, row form (4 float4) for it
+  const long n2 = (long)(npass - 1) * LG_BN + 32 * wave + 4 * (lane & 7);
+  float axe[16];
+  f32x4 axr[4];
   for (int u = 0; u < nsl; ++u) {
+    const bool last_pass = (u >> 3) == npass - 1;
     if (!full) {
       gl_wait_vm<0>();
+    } else if (dgelu && (u & 7) == 2) {
+      if (last_pass) gl_wait_vm<4>();  // the operands stay in flight
+      else gl_wait_vm<16>();
     } else if (u == 0) {
       if (nsl > 1) gl_wait_vm<13>();
       else gl_wait_vm<9>();
@@ -2434,6 +2444,17 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     __builtin_amdgcn_sched_barrier(0);
     if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
     const int t = u & 7;
+    if (dgelu && t == 1) {
+      if (!last_pass) {
+        const long cn = (u >> 3) * LG_BN + 32 * wave + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          axe[r] = LN.aux[(long)min(m0 + (r & 3) + 8 * (r >> 2) + 4 * h, P.M - 1) * ldw + cn];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) axr[i] = ld4(LN.aux + (long)min(m0 + (lane >> 3) + 8 * i, P.M - 1) * ldw + n2);
+      }
+    }
     const float* Bf = reinterpret_cast<const float*>(smem + (u & 1) * LB_B2);
     f32x4 fa[4], fb[4];
 #pragma unroll
@@ -2454,7 +2475,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
         const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m >= P.M) continue;
         float o = acc2[r];
-        if (dgelu) o *= gelu_erf_grad(LN.aux[(long)m * ldw + cn]);
+        if (dgelu) o *= gelu_erf_grad(axe[r]);
         st1g(LN.dout + (long)m * ldw + cn, o);
       }
 #pragma unroll
@@ -2464,16 +2485,14 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   __syncthreads();  // ring free: wave-private transposition scratch (8 x 5 KB) for row stores
   f32x4 rows[4];
   acc_to_rows(acc2, reinterpret_cast<float*>(smem) + wave * 32 * EPI_LD, lane, rows);
-  const long n2 = (long)(npass - 1) * LG_BN + 32 * wave + 4 * (lane & 7);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + (lane >> 3) + 8 * i;
     if (m >= P.M) continue;
     f32x4 o = rows[i];
     if (dgelu) {
-      const f32x4 ax = ld4(LN.aux + (long)m * ldw + n2);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(ax[j]);
+      for (int j = 0; j < 4; ++j) o[j] *= gelu_erf_grad(axr[i][j]);
     }
     st4(LN.dout + (long)m * ldw + n2, o);
   }
