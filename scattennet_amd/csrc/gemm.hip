@@ -1617,6 +1617,13 @@ bool ln_reg_default() {
   static const bool on = !(getenv("SCA_LNREG") && atoi(getenv("SCA_LNREG")) == 0);
   return on;
 }
+// SCA_LNB_R3=1: the chained input-gradient passes on a 3-stage B ring (147.5 KB of LDS; opt-in:
+// -0.17 % in the config 2 step, 3 alternated reps — the passes are not bound by the slice
+// latency, and the larger footprint keeps the side stream's kernels off those CUs)
+bool lnb_r3_default() {
+  static const bool on = getenv("SCA_LNB_R3") && atoi(getenv("SCA_LNB_R3")) == 1;
+  return on;
+}
 
 // ------------------------------------------------------------------------------ GEMM + LayerNorm
 // NT GEMM whose epilogue completes the post-LN block (keypoint_module.py:63-72, 99-109):
@@ -2171,6 +2178,10 @@ constexpr int LB_A2_OFF = 2 * LB_B2;
 constexpr int LB_RED_OFF = LB_A2_OFF + LB_BM * LB_A2_LD * 4;
 constexpr int LB_SMEM = LB_RED_OFF + 2 * 8 * 256 * 4 > LB_S * LB_STAGE ? LB_RED_OFF + 2 * 8 * 256 * 4
                                                                          : LB_S * LB_STAGE;
+// R3: a third phase-2 B stage after everything else (147.5 KB), so the chained passes' B
+// slices stream two slices ahead
+constexpr int LB_B3_OFF = LB_SMEM;
+constexpr int LB_SMEM3 = LB_B3_OFF + LB_B2;
 
 struct GemmLnbArgs {
   sca_gemm_problem p[SCA_GEMM_MAX_PROBLEMS];
@@ -2179,10 +2190,11 @@ struct GemmLnbArgs {
 
 // NC = 2: d_model = 512 as two 256-column halves (one continuous slice sequence, two
 // accumulators per wave), a 32 x 512 epilogue tile, no chained GEMM.
-template <int NC, bool REG = false>
+template <int NC, bool REG = false, bool R3 = false>
 __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   if constexpr (SCA_CRIT_PRIO > 0) __builtin_amdgcn_s_setprio(SCA_CRIT_PRIO);
-  __shared__ __attribute__((aligned(1024))) char smem[LB_SMEM];
+  static_assert(!R3 || (NC == 1 && LB_SMEM3 <= 160 * 1024), "LDS map (R3)");
+  __shared__ __attribute__((aligned(1024))) char smem[R3 ? LB_SMEM3 : LB_SMEM];
   constexpr int VS = NC * LG_BN + 8, NROW = NC * LG_BN;
   constexpr int RED_OFF = NC == 1 ? LB_RED_OFF : LB_BM * VS * 4;  // dgamma / dbeta wave partials
   static_assert(LB_B2 >= LB_BM * LG_VS * 4 && LB_RED_OFF + 2 * 8 * LG_BN * 4 <= LB_SMEM, "LDS map");
@@ -2348,10 +2360,11 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   const int npass = chain ? max(LN.npass, 1) : 0;
   const long ldw = LN.ldw ? LN.ldw : (long)LG_BN * npass;
   const float* pw = LN.wo + (long)(4 * wave) * ldw + 4 * lane;  // B pieces: k-rows 4*wave .. +3
+  auto stage_at = [&](int stage) { return smem + (R3 && stage == 2 ? LB_B3_OFF : stage * LB_B2); };
   auto dma2 = [&](int u, int stage) {
     const float* src = pw + (u >> 3) * LG_BN + (long)(32 * (u & 7)) * ldw;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) gl_dma(src + c * ldw, smem + stage * LB_B2 + (4 * wave + c) * LB_BROW);
+    for (int c = 0; c < 4; ++c) gl_dma(src + c * ldw, stage_at(stage) + (4 * wave + c) * LB_BROW);
   };
   if (chain) {
     __syncthreads();
@@ -2427,7 +2440,19 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
   f32x4 axr[4];
   for (int u = 0; u < nsl; ++u) {
     const bool last_pass = (u >> 3) == npass - 1;
-    if (!full) {
+    if constexpr (R3) {
+      // slice u was issued two slices back; younger: slice u+1's pieces (4), the GELU'
+      // operands issued behind slice u's or slice u+1's pieces (16 / 4 in the last pass), and
+      // the element-form stores of a pass that ended in between (16); the LayerNorm
+      // epilogue's 9 stores are younger than slices 0 and 1
+      const int t = u & 7;
+      if (!full || u == nsl - 1) gl_wait_vm<0>();
+      else if (u < 2) gl_wait_vm<13>();
+      else if (t < 2) gl_wait_vm<20>();
+      else if (t < 4 && dgelu && !last_pass) gl_wait_vm<20>();
+      else if (t < 4 && dgelu) gl_wait_vm<8>();
+      else gl_wait_vm<4>();
+    } else if (!full) {
       gl_wait_vm<0>();
     } else if (dgelu && (u & 7) == 2) {
       if (last_pass) gl_wait_vm<4>();  // the operands stay in flight
@@ -2442,7 +2467,11 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
+    if constexpr (R3) {
+      if (u + 2 < nsl) dma2(u + 2, (u + 2) % 3);  // into the stage slice u-1 left
+    } else {
+      if (u >= 1 && u + 1 < nsl) dma2(u + 1, (u + 1) & 1);  // into the stage slice u-1 left
+    }
     const int t = u & 7;
     if (dgelu && t == 1) {
       if (!last_pass) {
@@ -2455,7 +2484,7 @@ __global__ __launch_bounds__(512) void gemm_lnb_kernel(const GemmLnbArgs args) {
         for (int i = 0; i < 4; ++i) axr[i] = ld4(LN.aux + (long)min(m0 + (lane >> 3) + 8 * i, P.M - 1) * ldw + n2);
       }
     }
-    const float* Bf = reinterpret_cast<const float*>(smem + (u & 1) * LB_B2);
+    const float* Bf = reinterpret_cast<const float*>(stage_at(R3 ? u % 3 : u & 1));
     f32x4 fa[4], fb[4];
 #pragma unroll
     for (int g2 = 0; g2 < 4; ++g2) {
@@ -3167,7 +3196,11 @@ extern "C" int sca_gemm_lnb(int nprob, const sca_gemm_problem* probs, const sca_
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   bool reg = N == LG_BN && ln_reg_default();
   for (int i = 0; i < nprob; ++i) reg = reg && ln_reg_ok(probs[i], true);
-  if (reg) hipLaunchKernelGGL((gemm_lnb_kernel<1, true>), dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  bool chained = false;
+  for (int i = 0; i < nprob; ++i) chained = chained || a.ln[i].wo != nullptr;
+  if (reg && chained && lnb_r3_default())
+    hipLaunchKernelGGL((gemm_lnb_kernel<1, true, true>), dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
+  else if (reg) hipLaunchKernelGGL((gemm_lnb_kernel<1, true>), dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   else if (N == LG_BN) hipLaunchKernelGGL(gemm_lnb_kernel<1>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   else hipLaunchKernelGGL(gemm_lnb_kernel<2>, dim3((maxM + LB_BM - 1) / LB_BM, 1, nprob), dim3(512), 0, st, a);
   if (hipGetLastError() != hipSuccess) { sca_set_error("sca_gemm_lnb: launch failed"); return SCA_ERR_LAUNCH; }

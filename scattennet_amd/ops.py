@@ -441,6 +441,9 @@ def _chain_lns(nxt, G, M, like, gam, bet, ys, means, rstds):
     return lns
 
 
+_LNB_R3 = os.environ.get("SCA_LNB_R3", "0") == "1"  # the library's switch of the same name (names only)
+
+
 def gemm_lnb(probs, lnp):
     """Consumer backward: the NN input-gradient GEMMs `probs` (C = dL/dy of the LayerNorms
     `lnp`, N = 256) with those LayerNorms' backward fused (sca_gemm_lnb); the LN-input
@@ -467,7 +470,9 @@ def gemm_lnb(probs, lnp):
     if chain and _PROFILER:
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
     nc = probs[0].N // 256
-    with _timed(f"gemm_lnb_kernel<{nc}, {'true' if nc == 1 and _ln_reg(probs) else 'false'}>", flops):
+    reg = nc == 1 and _ln_reg(probs)
+    name = "gemm_lnb_kernel<1, true, true>" if reg and chain and _LNB_R3 else f"gemm_lnb_kernel<{nc}, {str(reg).lower()}>"
+    with _timed(name, flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
 
