@@ -471,7 +471,7 @@ def gemm_lnb(probs, lnp):
         flops += sum(2.0 * p.M * 256 * n2 for p in probs)
     nc = probs[0].N // 256
     reg = nc == 1 and _ln_reg(probs)
-    name = "gemm_lnb_kernel<1, true, true>" if reg and chain and _LNB_R3 else f"gemm_lnb_kernel<{nc}, {str(reg).lower()}>"
+    name = f"gemm_lnb_kernel<{nc}, {str(reg).lower()}, {str(bool(reg and chain and _LNB_R3)).lower()}>"
     with _timed(name, flops):
         L.check(lib.sca_gemm_lnb(len(probs), arr, larr, L.stream_handle()), "sca_gemm_lnb")
     return dv, part, nblk, dout
