@@ -979,8 +979,8 @@ def weight_grads(items, M=None, extra=None, ready=None, holdable=False):
     bias are the parameters (bias None / False: no bias gradient; True: a bias gradient
     without its parameter at hand).  bias_scale defaults to alpha; it differs when alpha
     scales the INPUT X (v from kv/2: dWv = dV^T (kv/2) but dbv = colsum(dV))."""
-    def run(defer=False):
-        out = _weight_grads(items)
+    def run(defer=False, sk=0):
+        out = _weight_grads(items, sk)
         params_produced([p for it in items for p in (it[3], it[4])])
         _run_extra(extra, defer)
         return out
@@ -1005,9 +1005,12 @@ def weight_grads(items, M=None, extra=None, ready=None, holdable=False):
             # only a backward that begins with the SCA blocks' sections holds (config 2); one that
             # begins elsewhere (config 3: fusion, residual network) forks every section
             _held.update(task=task, n=0, count=0, entries=[], hold=_hold_count() if holdable else 0)
+    late_sk = 0
     if _WGRAD_HOLD_FRAC > 0 and holdable:
         _held["count"] += 1
         hold = _held["hold"]
+        if _WGRAD_LATE_SK and hold > 0 and _held["count"] > _WGRAD_LATE_FROM * _held["last_total"]:
+            late_sk = _WGRAD_LATE_SK
         if _held["n"] < hold:
             # held: the gradients are allocated and returned now, their launches issued together
             # with the following held sections' at the last one's fork (or at the join).  The
@@ -1030,7 +1033,7 @@ def weight_grads(items, M=None, extra=None, ready=None, holdable=False):
     note_fork(side, main, "weight-gradient side stream")
     _record_on(side, items, extra)
     with torch.cuda.stream(side):
-        out = run(defer=_AFFINE_DEFER)
+        out = run(defer=_AFFINE_DEFER, sk=late_sk)
     _queue_join(main, side)
     return out
 
@@ -1070,6 +1073,14 @@ def _record_on(side, items, extra, outs=()):
 # backward's sections; the first backward holds none)
 _WGRAD_HOLD_FRAC = float(os.environ.get("SCA_WGRAD_HOLD", "0.45"))
 _WGRAD_HOLD_MERGE = os.environ.get("SCA_WGRAD_HOLD_MERGE", "1") != "0"
+# SCA_WGRAD_LATE_SK=k, SCA_WGRAD_LATE_FROM=f: in a backward that holds (one beginning with the
+# SCA blocks), the sections after the first f of the previous backward's — the ones whose
+# launches end up running alone after the main stream — at split-K k when their rule gave less
+# (768 workgroups instead of 512 for 16 x (256, 256): the whole chip when nothing runs beside
+# them).  Config 2: +0.31 % (f 0.5, 4 alternated reps), +0.19 % from the first non-held
+# section; config 3 (no hold, so not applied): -1.45 % if it were; 0 switches it off
+_WGRAD_LATE_SK = int(os.environ.get("SCA_WGRAD_LATE_SK", "3"))
+_WGRAD_LATE_FROM = float(os.environ.get("SCA_WGRAD_LATE_FROM", "0.5"))
 
 _held = {"task": None, "n": 0, "count": 0, "entries": [], "hold": 0, "last_total": 0}
 
@@ -1125,10 +1136,10 @@ def _flush_held(main, side, ready=None):
                 params_produced(ex[2])
 
 
-def _weight_grads(items):
+def _weight_grads(items, sk=0):
     """Allocate the gradients and launch the grouped split-K TN GEMMs -> [(dW, db)]."""
     out = _wgrad_alloc(items)
-    _wgrad_launch(_wgrad_specs(items, out))
+    _wgrad_launch(_wgrad_specs(items, out), sk)
     return out
 
 
@@ -1160,7 +1171,7 @@ def _wgrad_specs(items, out):
     return specs
 
 
-def _wgrad_launch(specs):
+def _wgrad_launch(specs, sk_late=0):
     """Grouped launches of the weight-gradient problems: equal (out, in, rows) shapes share a
     launch (up to GEMM_MAX_PROBLEMS), the kernel variant and split-K chosen per launch."""
     if not specs:
@@ -1199,6 +1210,8 @@ def _wgrad_launch(specs):
                     sk = _TNR_MIXED_SK
                 if _TNR_SK and Kr // _TNR_SK >= 256:
                     sk = _TNR_SK
+                if sk_late and sk < sk_late and Kr // sk_late >= 256:  # raise only
+                    sk = sk_late
             elif (len(sub) >= 8 and tiles >= 256) or tiles >= _TNK_TILES_PER_PROBLEM * len(sub):
                 # many-problem launches (an attention block's q/k/v/o of every stream) and big
                 # weights (an FFN's 768 x 256): the k-split outer-product kernel at split-K 2
