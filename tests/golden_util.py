@@ -8,12 +8,12 @@ import torch
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def manifest():
-    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+def manifest(fname="manifest.json"):
+    with open(os.path.join(GOLDEN, fname)) as f:
         return json.load(f)
 
 
-def load(name):
+def load(name, manifest_name="manifest.json"):
     z = np.load(os.path.join(GOLDEN, name + ".npz"))  # allow_pickle=False (default)
     fx = {"in": {}, "param": {}, "grad_in": {}, "grad_param": {}}
     for k in z.files:
@@ -28,7 +28,7 @@ def load(name):
             fx["grad_param"][k[11:]] = v
         else:
             fx[k] = v
-    fx["meta"] = manifest()["fixtures"][name]
+    fx["meta"] = manifest(manifest_name)["fixtures"][name]
     return fx
 
 

@@ -13,20 +13,21 @@ from tests.golden_util import close, load, manifest, rel_err
 TOL = 2e-5  # fp32 CPU vs fp32 CPU: only summation-order differences
 
 
-def _run(name, fn, grad_inputs):
-    fx = load(name)
-    params = {k: v.clone().requires_grad_(True) for k, v in fx["param"].items() if v.is_floating_point()}
-    inputs = {k: (v.clone().requires_grad_(True) if k in grad_inputs else v) for k, v in fx["in"].items()}
+def _run(name, fn, grad_inputs, manifest_name="manifest.json", tol=(TOL, TOL)):
+    fx = load(name, manifest_name)
+    f32 = lambda v: v.float() if v.is_floating_point() else v  # noqa: E731  (fp16 fixtures: fp32 oracle)
+    params = {k: f32(v).clone().requires_grad_(True) for k, v in fx["param"].items() if v.is_floating_point()}
+    inputs = {k: (f32(v).clone().requires_grad_(True) if k in grad_inputs else v) for k, v in fx["in"].items()}
     out = fn(params, inputs, fx["meta"])
-    assert rel_err(out, fx["out"]) < TOL
+    assert rel_err(out, fx["out"].float()) < tol[0]
     (out * fx["gout"]).sum().backward()
     for k in grad_inputs:
-        assert rel_err(inputs[k].grad, fx["grad_in"][k]) < TOL, k
-    gscale = max(float(g.abs().max()) for g in fx["grad_param"].values())
+        assert rel_err(inputs[k].grad, fx["grad_in"][k].float()) < tol[1], k
+    gscale = max(float(g.float().abs().max()) for g in fx["grad_param"].values())
     for k, g in fx["grad_param"].items():
         got = params[k].grad
         assert got is not None, k
-        assert close(got, g, TOL, gscale), (k, rel_err(got, g))
+        assert close(got, g.float(), tol[1], gscale), (k, rel_err(got, g.float()))
     # parameters the reference leaves without gradient must stay without gradient here
     for k, p in params.items():
         if k not in fx["grad_param"]:
@@ -109,3 +110,23 @@ def test_position_table_overflow_raises():
 def test_xstream_cfg1():
     """BASELINE config 1's x-coordinate stream (the CPU baseline's config-1 workload)."""
     _run("xstream_cfg1", lambda p, i, m: O.x_stream(p, "", i["keypoints"], i["mask"], m["cfg"]), ("keypoints",))
+
+
+# the reference computing in float16 (tests/golden/gen_golden_half.py) against the fp32 oracle
+# on the same (fp16-valued) parameters and inputs: fp16 rounding of every intermediate only —
+# the tolerances the GPU `.half()` modules are held to (tests/test_gpu_precision.py)
+HALF = (4e-3, 6e-3)
+
+
+def test_sca_stack_half_fixture():
+    _run("half_sca_L2", lambda p, i, m: O.sca(p, "", i["x_embed"], i["y_embed"], i["mask"], m["cfg"]),
+         ("x_embed", "y_embed"), "manifest_half.json", HALF)
+
+
+@pytest.mark.parametrize("kind", ["self_attn", "causal_attn"])
+def test_coordinate_attention_half_fixture(kind):
+    def fn(p, i, meta):
+        m = O.additive_key_mask(i["mask"]) if kind == "self_attn" else O.additive_causal_mask(i["mask"])
+        return O.coordinate_attention(p, "", i["coord_embed"], m, meta["cfg"]["attention_heads"], kind)
+
+    _run("half_coordattn_" + kind, fn, ("coord_embed",), "manifest_half.json", HALF)
