@@ -443,6 +443,11 @@ int sca_dropout(int nprob, const sca_dropout_problem* probs, long rows, int cols
 #define SCA_MASK_I16 8
 int sca_key_valid(const void* mask, int dtype, float* key_valid, long n, void* stream);
 
+/* p[0 .. n) = 0 (fp32): the gradient buffers a backward only partly writes (the position
+ * table's rows that no frame reads, model/layers.py LearningPositionEmbedding) — one launch
+ * in the captured step instead of an ATen fill.                                          */
+int sca_zero(float* p, long n, void* stream);
+
 /* Registers a device-resident step counter (or NULL) read by every dropout mask at run
  * time: effective seed = seed + counter * 0x9E3779B97F4A7C15.  A hipGraph that captures
  * the counter's increment then draws fresh masks on every replay although the seeds in

@@ -151,6 +151,7 @@ EXPORTS = {
     "sca_dropout": ([c_int, c_void_p, c_long, c_int, c_float, c_void_p], c_int),
     "sca_dropout_offset": ([c_void_p], c_int),
     "sca_key_valid": ([c_void_p, c_int, c_void_p, c_long, c_void_p], c_int),
+    "sca_zero": ([c_void_p, c_long, c_void_p], c_int),
     "sca_reduce_rows": ([c_int, c_void_p, c_int, c_int, c_int, c_long, c_long, c_int, c_void_p], c_int),
     "sca_coord_map_fwd": ([c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "sca_coord_map_bwd_chunks": ([c_int], c_int),

@@ -1186,6 +1186,33 @@ extern "C" int sca_key_valid(const void* mask, int dtype, float* key_valid, long
   return SCA_OK;
 }
 
+// p[0 .. n) = 0: float4 stores over the 16-byte-aligned body, scalar stores at the ends
+__global__ __launch_bounds__(256) void zero_kernel(float* p, long n, long head, long n4) {
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride)
+    st4(p + head + 4 * i, f32x4{0.f, 0.f, 0.f, 0.f});
+  const long tail = head + 4 * n4;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < head) p[e] = 0.f;
+  if (e < n - tail) p[tail + e] = 0.f;
+}
+
+extern "C" int sca_zero(float* p, long n, void* stream) {
+  if (n < 0 || (n > 0 && !p) || (reinterpret_cast<uintptr_t>(p) & 3)) {
+    sca_set_error("sca_zero: bad arguments (null or misaligned pointer, or n < 0)");
+    return SCA_ERR_ARG;
+  }
+  if (n == 0) return SCA_OK;
+  long head = (long)((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4;
+  if (head > n) head = n;
+  const long n4 = (n - head) / 4;
+  const long want = (n4 + 255) / 256;
+  const int blocks = (int)(want < 1 ? 1 : (want < 2048 ? want : 2048));
+  hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, n, head, n4);
+  if (hipGetLastError() != hipSuccess) { sca_set_error("sca_zero: launch failed"); return SCA_ERR_LAUNCH; }
+  return SCA_OK;
+}
+
 extern "C" int sca_normalize_parts(const float* kp_in, float* kp_out, const int* lengths, int B, int T, int K_all,
                                    const int* part_off, const int* part_idx, int nparts, void* stream) {
   if (B < 0 || T < 0 || K_all < 1 || K_all > NORM_KMAX || nparts < 0 || !kp_in || !kp_out || !lengths ||

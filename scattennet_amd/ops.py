@@ -1999,8 +1999,10 @@ class LayerNormAdd(Function):
         dtab = []
         if pos:
             B, T = x[0].shape[0], x[0].shape[1]
-            if _GRAD_SINK is None:
-                dtab = list(torch.zeros((G,) + tuple(tab[0].shape), device=tab[0].device).unbind(0))  # one fill
+            if _GRAD_SINK is None:  # one sca_zero launch for the G tables (rows no frame reads stay 0)
+                flat = torch.empty((G,) + tuple(tab[0].shape), device=tab[0].device)
+                L.check(L.lib().sca_zero(flat.data_ptr(), flat.numel(), L.stream_handle()), "sca_zero")
+                dtab = list(flat.unbind(0))
             else:
                 dtab = [param_grad_zeros(t) for t in tab]
             # d table[t + 2] = sum_b dv[b, t]

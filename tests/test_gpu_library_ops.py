@@ -175,3 +175,18 @@ def test_compiled_sca_stack_matches_eager():
     assert _rel(got[1], want[1]) < 1e-4 and _rel(got[2], want[2]) < 1e-4
     for k in want[3]:  # (k_proj.bias: analytically zero, compared at the noise level)
         assert float((got[3][k] - want[3][k]).abs().max()) <= 1e-4 * float(want[3][k].abs().max()) + 1e-6, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("off,n", [(0, 0), (0, 1), (1, 3), (3, 7), (0, 4096), (1, 4096 * 33 + 5), (2, 258 * 256 * 4)])
+def test_sca_zero_writes_exactly_its_range(off, n):
+    """sca_zero: p[0 .. n) = 0 at any 4-byte alignment (scalar head / tail around float4 stores),
+    nothing outside it touched — the position-table gradient's buffer in the captured step."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from scattennet_amd import _lib as L
+    buf = torch.full((off + n + 9,), float("nan"), device="cuda")
+    assert L.lib().sca_zero(buf.data_ptr() + 4 * off, n, L.stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(buf[off:off + n], torch.zeros(n, device="cuda"))
+    assert torch.isnan(buf[:off]).all() and torch.isnan(buf[off + n:]).all()
