@@ -719,13 +719,17 @@ __global__ __launch_bounds__(256, FB_OCC) void attn_bwd_fused_kernel(const BwdAr
   const uint32_t ebase = drop_row(b, a.H, h, Tq, Tk, 0);
 
   // own key tiles: K, V rows (B operands of S = Q K^T, dP = dO V^T) and K^T fragments
-  // (A operand of dQ^T = K^T dS^T: lane (d = kj, grp) holds K[16g + 4grp + r][d])
+  // (A operand of dQ^T = K^T dS^T: lane (d = kj, grp) holds K[16g + 4grp + r][d]).  Wave w
+  // owns tiles w, 15 - w, 7 - w, 8 + w: under the causal mask key tile g meets 16 - g query
+  // tiles, so every wave gets 34 tile pairs (the interleaved g = 4i + w gave wave 0 40 and
+  // wave 3 28, and the two workgroups of a CU put their waves 0 on the same SIMD)
+  auto own = [&](int i) { return i == 0 ? w : i == 1 ? 15 - w : i == 2 ? 7 - w : 8 + w; };
   float kreg[4][NS], vreg[4][NS], kadd[4];
   f32x4 ktf[4];
   const float* kb = P.k + (long)b * Tk * a.ldk + h * HD;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int g = 4 * i + w;
+    const int g = own(i);
     const int key = 16 * g + kj;
     const int kc = min(key, Tk - 1);
     const f32x4 kv = ld4(kb + (long)kc * a.ldk + NS * grp);
@@ -801,7 +805,7 @@ __global__ __launch_bounds__(256, FB_OCC) void attn_bwd_fused_kernel(const BwdAr
       f32x4 dq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int g = 4 * i + w;
+        const int g = own(i);
         if (16 * g >= Tk) continue;                    // wave-uniform: no keys in this tile
         if (CAUSAL && g > 4 * qb + t) continue;        // every key after every query of the tile
         f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = s_acc;
@@ -858,7 +862,7 @@ __global__ __launch_bounds__(256, FB_OCC) void attn_bwd_fused_kernel(const BwdAr
 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int key = 16 * (4 * i + w) + kj;
+    const int key = 16 * own(i) + kj;
     if (key < Tk) {
       st4(P.dk + ((long)b * Tk + key) * a.ldk + h * HD + 4 * grp, dk[i]);
       st4(P.dv + ((long)b * Tk + key) * a.ldv + h * HD + 4 * grp, dv[i] * P.dv_scale);
