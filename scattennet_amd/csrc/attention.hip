@@ -918,14 +918,19 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
   if (DROP) dm.init(P.drop_seed, P.drop_p, a.drop_off);
   const uint32_t ebase = drop_row(b, a.H, h, Tq, Tk, 0);
 
-  // own key tiles g = KW i + w: K, V rows (lane (kj, grp): d = 8 grp .. 8 grp + 7) and the K^T
-  // fragments of both 16-wide d blocks (lane (d = 16 dd + kj, grp): K[16g + 4grp + r][d])
+  // own key tiles (local to the block) w and 15 - w: under the causal mask local tile l meets
+  // 16 - l of the diagonal region's 16 query tiles, so every wave gets 17 there (w and 8 + w
+  // gave wave 0 24 and wave 7 10; the last key block is all diagonal region).  K, V rows (lane
+  // (kj, grp): d = 8 grp .. 8 grp + 7) and the K^T fragments of both 16-wide d blocks (lane
+  // (d = 16 dd + kj, grp): K[16g + 4grp + r][d])
+  static_assert(TPW == 2, "two key tiles per wave");
+  auto own = [&](int i) { return i == 0 ? w : KBLK / 16 - 1 - w; };
   float kreg[TPW][NS], vreg[TPW][NS], kadd[TPW];
   f32x4 ktf[TPW][ND];
   const float* kb = P.k + (long)b * Tk * a.ldk + h * HD;
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    const int key = k0 + 16 * (KW * i + w) + kj;
+    const int key = k0 + 16 * own(i) + kj;
     const int kc = min(key, Tk - 1);
 #pragma unroll
     for (int s = 0; s < NS; s += 4) {
@@ -941,7 +946,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
     for (int dd = 0; dd < ND; ++dd)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        ktf[i][dd][j] = kb[(long)min(k0 + 16 * (KW * i + w) + 4 * grp + j, Tk - 1) * a.ldk + 16 * dd + kj];
+        ktf[i][dd][j] = kb[(long)min(k0 + 16 * own(i) + 4 * grp + j, Tk - 1) * a.ldk + 16 * dd + kj];
     kadd[i] = key_add(kv_load(P.key_valid, b, key, Tk), false, key, Tk, plus2);
   }
   f32x4 dk[TPW][ND], dv[TPW][ND];
@@ -1034,7 +1039,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
     for (int dd = 0; dd < ND; ++dd) dq[dd] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-      const int g = (k0 >> 4) + KW * i + w;  // global 16-key tile index
+      const int g = (k0 >> 4) + own(i);  // global 16-key tile index
       if (GEN && 16 * g >= Tk) continue;      // wave-uniform: no keys in this tile
       if (GEN && CAUSAL && g > qt) continue;  // every key after every query of the tile
       f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = s_acc;
@@ -1076,7 +1081,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-      const int g = (k0 >> 4) + KW * i + w;
+      const int g = (k0 >> 4) + own(i);
       if (GEN && 16 * g >= Tk) continue;
       if (GEN && CAUSAL && g > qt) continue;
       const f32x4 dsv = ld4(&dSw[w][i][kj * FB_TS + 4 * grp]);
@@ -1120,7 +1125,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kblk_kernel(const BwdArgs
 
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    const int key = k0 + 16 * (KW * i + w) + kj;
+    const int key = k0 + 16 * own(i) + kj;
     if (key < Tk) {
 #pragma unroll
       for (int dd = 0; dd < ND; ++dd) {
