@@ -3,7 +3,7 @@ scattennet_amd/csrc stamps): per-workgroup s_memrealtime at entry, main loop don
 done, first chained pass done, end — for the workload's out-projection + fc1-chain and
 fc2 + qkv-chain launches (4 streams x 2048 rows, 32-row tiles).
 
-    python tools/gemm_ln_stamps.py
+    python tools/gemm_ln_stamps.py [other_stamps_build.so]
 """
 import ctypes
 import os
@@ -15,7 +15,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scattennet_amd import _lib as L, ops  # noqa: E402
 
-L.LIB_PATH = os.path.join(os.path.dirname(L.LIB_PATH), "libscatten_hip_stamps.so")
+# the stamps build (or, A/B, another stamps build given as the first argument)
+L.LIB_PATH = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(L.LIB_PATH), "libscatten_hip_stamps.so")
 
 
 def run_case(name, G, M, K, passes):
