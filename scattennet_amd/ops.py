@@ -1071,16 +1071,17 @@ def _record_on(side, items, extra, outs=()):
 # grouped launch) at the n-th section's fork — one fork marker instead of n, fuller launches
 # SCA_WGRAD_HOLD=n (an integer: n sections) or a fraction f < 1 (the first f of the previous
 # backward's sections; the first backward holds none)
-_WGRAD_HOLD_FRAC = float(os.environ.get("SCA_WGRAD_HOLD", "0.45"))
+_WGRAD_HOLD_FRAC = float(os.environ.get("SCA_WGRAD_HOLD", "0.5"))
 _WGRAD_HOLD_MERGE = os.environ.get("SCA_WGRAD_HOLD_MERGE", "1") != "0"
 # SCA_WGRAD_LATE_SK=k, SCA_WGRAD_LATE_FROM=f: in a backward that holds (one beginning with the
 # SCA blocks), the sections after the first f of the previous backward's — the ones whose
 # launches end up running alone after the main stream — at split-K k when their rule gave less
 # (768 workgroups instead of 512 for 16 x (256, 256): the whole chip when nothing runs beside
 # them).  Config 2: +0.31 % (f 0.5, 4 alternated reps), +0.19 % from the first non-held
-# section; config 3 (no hold, so not applied): -1.45 % if it were; 0 switches it off
+# section; with the hold at 0.5: f 0.5 / 0.55 / 0.6 within 0.1 % of each other; config 3 (no
+# hold, so not applied): -1.45 % if it were; 0 switches it off
 _WGRAD_LATE_SK = int(os.environ.get("SCA_WGRAD_LATE_SK", "3"))
-_WGRAD_LATE_FROM = float(os.environ.get("SCA_WGRAD_LATE_FROM", "0.5"))
+_WGRAD_LATE_FROM = float(os.environ.get("SCA_WGRAD_LATE_FROM", "0.55"))
 
 _held = {"task": None, "n": 0, "count": 0, "entries": [], "hold": 0, "last_total": 0}
 
